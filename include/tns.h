@@ -1,0 +1,190 @@
+/*
+ * tns.h -- C ABI of libtns, the MI355X (gfx950) twist-and-shout prover hot path.
+ *
+ * This is the drop-in boundary: the entry points a Rust `extern "C"` block (see
+ * INTEGRATION.md) binds beneath the unchanged signatures of the reference crate
+ * `twist-and-shout` (/root/reference).  Each function cites the reference
+ * interface it replaces.
+ *
+ * Conventions
+ *  - Field elements (Fr, Fq) are `uint64_t[4]`, little-endian, Montgomery form
+ *    with R = 2^256: the in-memory layout of arkworks 0.4 `Fp256`, so a Rust
+ *    `&[Fr]` can be passed as `*const u64` without conversion.
+ *  - G1 affine inputs are `uint64_t[8]` = (x, y), Montgomery Fq; the all-zero
+ *    pair encodes the identity.
+ *  - G1 outputs are `uint64_t[12]` = arkworks `G1Projective` (Jacobian X, Y, Z),
+ *    normalised: Z = 1 (Montgomery one) for finite points, (1, 1, 0) for the
+ *    identity (ark-ec 0.4 `Projective::zero()`).
+ *  - All pointers are caller-owned host memory, not retained after return.
+ *    Every call is synchronous (stream-synchronised before return) and
+ *    serialised per context; distinct contexts may be used from distinct threads.
+ *  - Status codes mirror `TwistAndShoutError` (src/lib.rs:59-78); device
+ *    failures are >= 100.  `tns_last_error()` returns a thread-local message.
+ */
+#ifndef TNS_H
+#define TNS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  TNS_OK = 0,
+  TNS_ERR_INVALID_PARAMETERS = 1, /* TwistAndShoutError::InvalidParameters */
+  TNS_ERR_PROOF_GENERATION = 2,   /* ::ProofGeneration */
+  TNS_ERR_PROOF_VERIFICATION = 3, /* ::ProofVerification */
+  TNS_ERR_COMMITMENT = 4,         /* ::Commitment */
+  TNS_ERR_POLYNOMIAL = 5,         /* ::Polynomial */
+  TNS_ERR_SUMCHECK = 6,           /* ::SumCheck */
+  TNS_ERR_DEVICE = 100,           /* HIP runtime failure */
+  TNS_ERR_NO_DEVICE = 101,        /* no gfx950 device visible */
+  TNS_ERR_OOM = 102               /* device allocation failed */
+};
+
+#define TNS_MAX_ROUNDS 40
+
+typedef struct tns_ctx tns_ctx;
+typedef struct tns_srs tns_srs;
+typedef struct tns_transcript tns_transcript;
+
+/* Output of setup_params (src/utils.rs:79-131). */
+typedef struct {
+  uint64_t log_size;
+  uint64_t max_operations;  /* 1 << (log_size + 2)                    (src/utils.rs:80)      */
+  uint64_t num_powers;      /* next_pow2(max_operations) + 1 SRS points (src/utils.rs:89-96) */
+  uint64_t tau[4];          /* CommitmentParams.tau (Montgomery)      (src/utils.rs:84,107)  */
+  uint8_t fiat_shamir_seed[32];                                   /* (src/utils.rs:101-102) */
+} tns_params;
+
+/*
+ * One proof.  Twist (src/twist.rs:76-89): commitments = {address, value}.
+ * Shout (src/shout.rs:64-79): commitments = {table, index}.  The trailing
+ * fields are diagnostics the reference computes but does not return.
+ */
+typedef struct {
+  uint64_t commitments[2][12];                      /* KZGCommitmentValue x2 */
+  uint32_t num_rounds;                              /* SumCheckProof rounds = log2(padded ops) */
+  uint32_t num_openings;                            /* 0 (no challenges) or 2 */
+  uint64_t round_polynomials[TNS_MAX_ROUNDS][4][4]; /* SumCheckProof.round_polynomials */
+  uint64_t final_evaluation[4];                     /* SumCheckProof.final_evaluation */
+  uint64_t opening_proofs[2][12];                   /* Vec<KZGProof> */
+  uint64_t final_evaluations[2][4];                 /* Vec<FieldElement> */
+  /* diagnostics */
+  uint64_t opening_point[4];                        /* challenges[0] */
+  uint64_t sumcheck_challenges[TNS_MAX_ROUNDS][4];
+  uint64_t final_mle_evals[3][4];                   /* MLE values at the sum-check point */
+} tns_proof;
+
+/* A degree <= 3 product term of a sum-check composition: coeff * prod T[tables[j]]
+ * (tables[j] = -1 for unused slots). */
+typedef struct {
+  uint64_t coeff[4];
+  int32_t tables[3];
+  int32_t pad;
+} tns_term;
+
+/* ---------------------------------------------------------------- library */
+const char *tns_last_error(void);
+int tns_version(void);
+/* Number of visible HIP devices (0 if none); never fails. */
+int tns_device_count(void);
+
+/* ---------------------------------------------------------------- context */
+int tns_ctx_create(int device, tns_ctx **out);
+void tns_ctx_destroy(tns_ctx *ctx);
+int tns_ctx_synchronize(tns_ctx *ctx);
+
+/* ---------------------------------------------------------------- setup / SRS */
+/* setup_params(log_size) (src/utils.rs:79-131): derives tau and the FS seed from
+ * ChaCha20Rng([42;32]) on the host and generates the `num_powers` G1 powers of tau
+ * on the device.  *srs_out may be NULL to skip SRS generation. */
+int tns_setup_params(tns_ctx *ctx, unsigned log_size, tns_params *out, tns_srs **srs_out);
+/* Upload an externally built CommitmentParams.g1_powers (affine, n points). */
+int tns_srs_upload(tns_ctx *ctx, const uint64_t *g1_affine, size_t n, tns_srs **out);
+/* Copy points [0, n) of the SRS to host memory (affine uint64_t[8] each). */
+int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_affine_out, size_t n);
+size_t tns_srs_len(const tns_srs *srs);
+void tns_srs_destroy(tns_srs *srs);
+
+/* ---------------------------------------------------------------- KZG (src/commitments.rs) */
+/* CommitmentScheme::commit for KZGCommitment (src/commitments.rs:162-180).
+ * n > srs_len -> TNS_ERR_COMMITMENT ("Polynomial degree exceeds setup size"). */
+int tns_kzg_commit(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, size_t n,
+                   uint64_t out_proj[12]);
+/* CommitmentScheme::open (src/commitments.rs:182-199): value = P(z) (Horner,
+ * :305-313) and proof = commit((P - v) / (x - z)) (:317-375). n <= 1 -> identity proof. */
+int tns_kzg_open(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, size_t n,
+                 const uint64_t z[4], uint64_t value[4], uint64_t proof_proj[12]);
+/* KZGCommitmentValue::hash (src/commitments.rs:73-84).  Host only. */
+int tns_commitment_hash(const uint64_t proj[12], uint64_t out[4]);
+/* Raw MSM: sum_i scalars[i] * points[i] over the first n SRS points. */
+int tns_msm(tns_ctx *ctx, const tns_srs *srs, const uint64_t *scalars, size_t n,
+            uint64_t out_proj[12]);
+
+/* ---------------------------------------------------------------- polynomials */
+/* poly_utils::lagrange_interpolate over the nodes 0..n-1 (src/polynomials.rs:301-352,
+ * as called by vector_to_polynomial, src/twist.rs:307-315): the n monomial
+ * coefficients of the unique interpolant, computed exactly in O(n log^2 n). */
+int tns_interpolate_consecutive(tns_ctx *ctx, const uint64_t *y, size_t n, uint64_t *coeffs);
+/* MultilinearExtension::evaluate (src/polynomials.rs:85-103); variable j <-> index bit j. */
+int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv, const uint64_t *point,
+                     uint64_t out[4]);
+/* MultilinearExtension::partial_evaluate (src/polynomials.rs:126-161): binds the
+ * first k (least-significant) variables; out has 2^(nv-k) entries. */
+int tns_mle_partial_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv,
+                             const uint64_t *fixed, unsigned k, uint64_t *out);
+
+/* ---------------------------------------------------------------- transcript (src/utils.rs:134-204) */
+tns_transcript *tns_transcript_new(const uint8_t seed[32]);
+void tns_transcript_free(tns_transcript *t);
+void tns_transcript_append_field_element(tns_transcript *t, const uint8_t *label, size_t label_len,
+                                         const uint64_t x[4]);
+void tns_transcript_append_field_elements(tns_transcript *t, const uint8_t *label,
+                                          size_t label_len, const uint64_t *xs, size_t n);
+void tns_transcript_challenge_field_element(tns_transcript *t, const uint8_t *label,
+                                            size_t label_len, uint64_t out[4]);
+
+/* ---------------------------------------------------------------- sum-check (src/sumcheck.rs:56-110) */
+/* SumCheck::prove for the closure x -> sum_t coeff_t * prod_j MLE(T_{t,j})(x) over n_tables
+ * MLE tables of 2^nv entries each (degree <= 3 per variable, as the reference's 4-point
+ * round interpolation assumes).  rounds_out: nv x 4 Fr; challenges_out: nv Fr (nullable). */
+int tns_sumcheck_prove(tns_ctx *ctx, const uint64_t *const *tables, int n_tables, unsigned nv,
+                       const uint64_t claimed_sum[4], const tns_term *terms, int n_terms,
+                       tns_transcript *transcript, uint64_t *rounds_out, uint64_t final_out[4],
+                       uint64_t *challenges_out);
+
+/* ---------------------------------------------------------------- protocols */
+/* Twist::prove (src/twist.rs:107-252).  The MemoryTrace's operations as SoA:
+ * addr[i] (usize address), value[i] (Fr), is_write[i] (1 = Write, 0 = Read). */
+int tns_twist_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
+                    const uint64_t *addr, const uint64_t *value, const uint8_t *is_write,
+                    size_t n_ops, tns_proof *out);
+/* Shout::prove (src/shout.rs:97-222).  LookupTable.entries (Fr) and the lookup
+ * indices (usize). */
+int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
+                    const uint64_t *entries, size_t n_entries, const uint64_t *indices,
+                    size_t n_lookups, tns_proof *out);
+
+/* ---------------------------------------------------------------- host utilities (no device) */
+/* Batch conversions between integers and Montgomery-form Fr / Fq (multi-threaded). */
+void tns_fr_from_u64(const uint64_t *in, size_t n, uint64_t *out_mont);
+void tns_fr_from_canonical(const uint64_t *in, size_t n, uint64_t *out_mont);
+void tns_fr_to_canonical(const uint64_t *in_mont, size_t n, uint64_t *out);
+void tns_fq_to_canonical(const uint64_t *in_mont, size_t n, uint64_t *out);
+/* The synthetic read/write trace of ProtocolBenchmarks (src/benchmarks.rs:88-99):
+ * op i writes Fr(42 i) to i % memory_size when i % 3 == 0, else reads (i / 2) % memory_size
+ * and records the current memory value.  value_u64 holds the values as integers. */
+int tns_bench_trace(size_t memory_size, size_t n_ops, uint64_t *addr, uint64_t *value_u64,
+                    uint8_t *is_write);
+
+/* Wall-clock breakdown of the last prove on this context (milliseconds):
+ * [0] H2D, [1] interpolation, [2] commit MSMs, [3] sum-check, [4] open, [5] total. */
+int tns_last_prove_timing(tns_ctx *ctx, double out_ms[6]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TNS_H */

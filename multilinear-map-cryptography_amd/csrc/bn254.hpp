@@ -1,0 +1,440 @@
+// bn254.hpp -- BN254 Fr / Fq Montgomery arithmetic and G1 group law for gfx950 (and host).
+//
+// Layout: a field element is 8 x u32 little-endian limbs in Montgomery form with
+// R = 2^256 -- byte-identical to arkworks' `Fp256` ([u64; 4] Montgomery), so
+// buffers cross the C ABI without conversion (src/utils.rs:14 FieldElement = ark_bn254::Fr).
+//
+// Multiplication is CIOS Montgomery with the "no-carry" shortcut (the top limb of
+// both moduli is < 2^31 - 1), built on 32x32+64 -> 64 multiply-adds, which hipcc
+// lowers to v_mad_u64_u32 on CDNA4.
+//
+// G1: y^2 = x^3 + 3 over Fq (ark-bn254 0.4.0).  Bucket sums use XYZZ coordinates
+// (x = X/ZZ, y = Y/ZZZ; identity <=> ZZ == 0), affine SRS points are (x, y) with
+// the all-zero pair standing for the identity.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define TNS_HD __host__ __device__ __forceinline__
+#define TNS_DEV __device__ __forceinline__
+#else
+#define TNS_HD inline
+#define TNS_DEV inline
+#endif
+
+namespace tns {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+struct FrCfg {
+  static constexpr u32 M[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                               0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr u32 ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                 0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr u32 R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+  static constexpr u32 INV = 0xefffffffu;
+};
+struct FqCfg {
+  static constexpr u32 M[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                               0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+  static constexpr u32 ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                 0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+  static constexpr u32 R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+  static constexpr u32 INV = 0xe4866389u;
+};
+
+template <class C>
+struct alignas(16) Fp {
+  u32 v[8];
+
+  TNS_HD static Fp zero() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = 0;
+    return r;
+  }
+  TNS_HD static Fp one() {
+    Fp r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = C::ONE[i];
+    return r;
+  }
+  TNS_HD bool is_zero() const {
+    u32 acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i];
+    return acc == 0;
+  }
+  TNS_HD bool operator==(const Fp &o) const {
+    u32 acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc |= v[i] ^ o.v[i];
+    return acc == 0;
+  }
+  TNS_HD bool operator!=(const Fp &o) const { return !(*this == o); }
+};
+
+typedef Fp<FrCfg> Fr;
+typedef Fp<FqCfg> Fq;
+
+// ---------------------------------------------------------------- raw 256-bit helpers
+// r = a - M if a >= M (a < 2M assumed)
+template <class C>
+TNS_HD void reduce_once(Fp<C> &a) {
+  u32 t[8];
+  u64 br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 d = (u64)a.v[i] - C::M[i] - br;
+    t[i] = (u32)d;
+    br = (d >> 32) & 1;
+  }
+  if (!br) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) a.v[i] = t[i];
+  }
+}
+
+template <class C>
+TNS_HD Fp<C> add(const Fp<C> &a, const Fp<C> &b) {
+  Fp<C> r;
+  u64 c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    c += (u64)a.v[i] + b.v[i];
+    r.v[i] = (u32)c;
+    c >>= 32;
+  }
+  reduce_once(r);  // a + b < 2M < 2^256: no carry out of limb 7
+  return r;
+}
+
+template <class C>
+TNS_HD Fp<C> sub(const Fp<C> &a, const Fp<C> &b) {
+  Fp<C> r;
+  u64 br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 d = (u64)a.v[i] - b.v[i] - br;
+    r.v[i] = (u32)d;
+    br = (d >> 32) & 1;
+  }
+  if (br) {
+    u64 c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c += (u64)r.v[i] + C::M[i];
+      r.v[i] = (u32)c;
+      c >>= 32;
+    }
+  }
+  return r;
+}
+
+template <class C>
+TNS_HD Fp<C> neg(const Fp<C> &a) {
+  if (a.is_zero()) return a;
+  Fp<C> r;
+  u64 br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 d = (u64)C::M[i] - a.v[i] - br;
+    r.v[i] = (u32)d;
+    br = (d >> 32) & 1;
+  }
+  return r;
+}
+
+template <class C>
+TNS_HD Fp<C> dbl(const Fp<C> &a) {
+  return add(a, a);
+}
+
+// CIOS Montgomery product, no-carry variant (top modulus limb < 2^31 - 1).
+template <class C>
+TNS_HD Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
+  u32 t[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const u32 bi = b.v[i];
+    u64 A = (u64)a.v[0] * bi + t[0];
+    const u32 m = (u32)A * C::INV;
+    u64 Cc = (u64)m * C::M[0] + (u32)A;
+#pragma unroll
+    for (int j = 1; j < 8; j++) {
+      A = (u64)a.v[j] * bi + ((u64)t[j] + (A >> 32));
+      Cc = (u64)m * C::M[j] + ((u64)(u32)A + (Cc >> 32));
+      t[j - 1] = (u32)Cc;
+    }
+    t[7] = (u32)((A >> 32) + (Cc >> 32));
+  }
+  Fp<C> r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = t[i];
+  reduce_once(r);
+  return r;
+}
+
+template <class C>
+TNS_HD Fp<C> sqr(const Fp<C> &a) {
+  return mul(a, a);
+}
+
+// multiply by a small constant via additions
+template <class C>
+TNS_HD Fp<C> mul3(const Fp<C> &a) {
+  return add(add(a, a), a);
+}
+
+template <class C>
+TNS_HD Fp<C> to_mont(const Fp<C> &canonical) {
+  Fp<C> r2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r2.v[i] = C::R2[i];
+  return mul(canonical, r2);
+}
+
+template <class C>
+TNS_HD Fp<C> from_mont(const Fp<C> &a) {
+  Fp<C> one = Fp<C>::zero();
+  one.v[0] = 1;
+  return mul(a, one);
+}
+
+template <class C>
+TNS_HD Fp<C> from_u64(u64 x) {
+  Fp<C> c = Fp<C>::zero();
+  c.v[0] = (u32)x;
+  c.v[1] = (u32)(x >> 32);
+  return to_mont(c);
+}
+
+// a^e for a 256-bit exponent given as 8 limbs (square-and-multiply, MSB first)
+template <class C>
+TNS_HD Fp<C> pow_limbs(const Fp<C> &a, const u32 e[8]) {
+  Fp<C> acc = Fp<C>::one();
+  for (int i = 255; i >= 0; i--) {
+    acc = sqr(acc);
+    if ((e[i >> 5] >> (i & 31)) & 1) acc = mul(acc, a);
+  }
+  return acc;
+}
+
+template <class C>
+TNS_HD Fp<C> pow_u64(const Fp<C> &a, u64 e) {
+  Fp<C> acc = Fp<C>::one(), base = a;
+  while (e) {
+    if (e & 1) acc = mul(acc, base);
+    base = sqr(base);
+    e >>= 1;
+  }
+  return acc;
+}
+
+// Fermat inverse (a^(M-2)); inverse of zero is zero.
+template <class C>
+TNS_HD Fp<C> inv(const Fp<C> &a) {
+  u32 e[8];
+  u64 br = 2;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    u64 d = (u64)C::M[i] - br;
+    e[i] = (u32)d;
+    br = (d >> 32) & 1;
+  }
+  return pow_limbs(a, e);
+}
+
+// canonical-integer comparison helpers (operate on from_mont'ed values)
+template <class C>
+TNS_HD bool geq_raw(const u32 a[8], const u32 b[8]) {
+  for (int i = 7; i >= 0; i--) {
+    if (a[i] > b[i]) return true;
+    if (a[i] < b[i]) return false;
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------- G1
+struct alignas(16) G1Affine {  // identity <=> x == y == 0
+  Fq x, y;
+  TNS_HD bool is_inf() const { return x.is_zero() && y.is_zero(); }
+};
+
+struct alignas(16) G1Xyzz {  // identity <=> zz == 0
+  Fq x, y, zz, zzz;
+  TNS_HD static G1Xyzz inf() {
+    G1Xyzz r;
+    r.x = Fq::one();
+    r.y = Fq::one();
+    r.zz = Fq::zero();
+    r.zzz = Fq::zero();
+    return r;
+  }
+  TNS_HD bool is_inf() const { return zz.is_zero(); }
+};
+
+struct alignas(16) G1Jac {  // arkworks G1Projective layout (Jacobian); identity <=> z == 0
+  Fq x, y, z;
+};
+
+TNS_HD G1Affine g1_neg(const G1Affine &p) {
+  G1Affine r;
+  r.x = p.x;
+  r.y = neg(p.y);
+  return r;
+}
+
+// dbl-2008-s-1 (a = 0)
+TNS_HD G1Xyzz xyzz_dbl(const G1Xyzz &p) {
+  if (p.is_inf() || p.y.is_zero()) return G1Xyzz::inf();
+  Fq U = dbl(p.y);
+  Fq V = sqr(U);
+  Fq W = mul(U, V);
+  Fq S = mul(p.x, V);
+  Fq M = mul3(sqr(p.x));
+  G1Xyzz r;
+  r.x = sub(sqr(M), dbl(S));
+  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.zz = mul(V, p.zz);
+  r.zzz = mul(W, p.zzz);
+  return r;
+}
+
+// mdbl-2008-s-1: double an affine point
+TNS_HD G1Xyzz xyzz_mdbl(const G1Affine &p) {
+  if (p.is_inf() || p.y.is_zero()) return G1Xyzz::inf();
+  Fq U = dbl(p.y);
+  Fq V = sqr(U);
+  Fq W = mul(U, V);
+  Fq S = mul(p.x, V);
+  Fq M = mul3(sqr(p.x));
+  G1Xyzz r;
+  r.x = sub(sqr(M), dbl(S));
+  r.y = sub(mul(M, sub(S, r.x)), mul(W, p.y));
+  r.zz = V;
+  r.zzz = W;
+  return r;
+}
+
+// madd-2008-s: XYZZ += affine
+TNS_HD G1Xyzz xyzz_madd(const G1Xyzz &p, const G1Affine &q) {
+  if (q.is_inf()) return p;
+  if (p.is_inf()) {
+    G1Xyzz r;
+    r.x = q.x;
+    r.y = q.y;
+    r.zz = Fq::one();
+    r.zzz = Fq::one();
+    return r;
+  }
+  Fq U2 = mul(q.x, p.zz);
+  Fq S2 = mul(q.y, p.zzz);
+  Fq P = sub(U2, p.x);
+  Fq R = sub(S2, p.y);
+  if (P.is_zero()) {
+    if (R.is_zero()) return xyzz_mdbl(q);
+    return G1Xyzz::inf();
+  }
+  Fq PP = sqr(P);
+  Fq PPP = mul(P, PP);
+  Fq Q = mul(p.x, PP);
+  G1Xyzz r;
+  r.x = sub(sub(sqr(R), PPP), dbl(Q));
+  r.y = sub(mul(R, sub(Q, r.x)), mul(p.y, PPP));
+  r.zz = mul(p.zz, PP);
+  r.zzz = mul(p.zzz, PPP);
+  return r;
+}
+
+// add-2008-s: XYZZ + XYZZ
+TNS_HD G1Xyzz xyzz_add(const G1Xyzz &p, const G1Xyzz &q) {
+  if (q.is_inf()) return p;
+  if (p.is_inf()) return q;
+  Fq U1 = mul(p.x, q.zz);
+  Fq U2 = mul(q.x, p.zz);
+  Fq S1 = mul(p.y, q.zzz);
+  Fq S2 = mul(q.y, p.zzz);
+  Fq P = sub(U2, U1);
+  Fq R = sub(S2, S1);
+  if (P.is_zero()) {
+    if (R.is_zero()) return xyzz_dbl(p);
+    return G1Xyzz::inf();
+  }
+  Fq PP = sqr(P);
+  Fq PPP = mul(P, PP);
+  Fq Q = mul(U1, PP);
+  G1Xyzz r;
+  r.x = sub(sub(sqr(R), PPP), dbl(Q));
+  r.y = sub(mul(R, sub(Q, r.x)), mul(S1, PPP));
+  r.zz = mul(mul(p.zz, q.zz), PP);
+  r.zzz = mul(mul(p.zzz, q.zzz), PPP);
+  return r;
+}
+
+TNS_HD G1Xyzz xyzz_from_affine(const G1Affine &a) {
+  if (a.is_inf()) return G1Xyzz::inf();
+  G1Xyzz r;
+  r.x = a.x;
+  r.y = a.y;
+  r.zz = Fq::one();
+  r.zzz = Fq::one();
+  return r;
+}
+
+// k * p for a small non-negative integer k (double-and-add)
+TNS_HD G1Xyzz xyzz_mul_small(const G1Xyzz &p, u64 k) {
+  G1Xyzz acc = G1Xyzz::inf();
+  for (int i = 63; i >= 0; i--) {
+    acc = xyzz_dbl(acc);
+    if ((k >> i) & 1) acc = xyzz_add(acc, p);
+  }
+  return acc;
+}
+
+// XYZZ -> affine (one field inversion)
+TNS_HD G1Affine xyzz_to_affine(const G1Xyzz &p) {
+  G1Affine r;
+  if (p.is_inf()) {
+    r.x = Fq::zero();
+    r.y = Fq::zero();
+    return r;
+  }
+  Fq izzz = inv(p.zzz);         // 1/ZZZ
+  Fq iz = mul(izzz, p.zz);      // ZZ/ZZZ = 1/z  (z = ZZZ/ZZ)
+  Fq izz = sqr(iz);             // 1/ZZ
+  r.x = mul(p.x, izz);
+  r.y = mul(p.y, izzz);
+  return r;
+}
+
+// affine -> arkworks G1Projective (Jacobian, Z = 1; identity = (1, 1, 0))
+TNS_HD G1Jac affine_to_jac(const G1Affine &a) {
+  G1Jac j;
+  if (a.is_inf()) {
+    j.x = Fq::one();
+    j.y = Fq::one();
+    j.z = Fq::zero();
+  } else {
+    j.x = a.x;
+    j.y = a.y;
+    j.z = Fq::one();
+  }
+  return j;
+}
+
+TNS_HD bool g1_on_curve(const G1Affine &a) {
+  if (a.is_inf()) return true;
+  Fq y2 = sqr(a.y);
+  Fq x3 = mul(sqr(a.x), a.x);
+  Fq three = from_u64<FqCfg>(3);
+  return y2 == add(x3, three);
+}
+
+}  // namespace tns

@@ -1,0 +1,172 @@
+// common.hpp -- shared host-side plumbing for libtns: status codes, HIP error
+// checks, grow-only device buffers, and the per-device context.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/tns.h"
+#include "bn254.hpp"
+
+namespace tns {
+
+// A thrown tns::Error carries one of the TNS_* status codes of include/tns.h
+// (mirroring TwistAndShoutError, src/lib.rs:59-78) across the C++ layer; the
+// C-ABI entry points catch it and store the message for tns_last_error().
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string &msg);
+
+#define TNS_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t _e = (call);                                                            \
+    if (_e != hipSuccess)                                                              \
+      throw ::tns::Error(TNS_ERR_DEVICE, std::string("HIP error ") + hipGetErrorString(_e) + \
+                                             " at " __FILE__ ":" + std::to_string(__LINE__)); \
+  } while (0)
+
+#define TNS_LAUNCH_CHECK() TNS_HIP(hipGetLastError())
+
+// Grow-only device allocation (never shrinks; freed with the context).
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf &) = delete;
+  DevBuf &operator=(const DevBuf &) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void *ensure(size_t n) {
+    if (n <= bytes && p) return p;
+    release();
+    size_t want = n ? n : 16;
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      throw Error(TNS_ERR_OOM, "hipMalloc of " + std::to_string(want) + " bytes failed: " +
+                                   hipGetErrorString(e));
+    }
+    bytes = want;
+    return p;
+  }
+  template <class T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+// Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).
+struct InterpPlan {
+  unsigned log_n = 0;   // N = 2^log_n
+  DevBuf fact, inv_fact;            // k!, 1/k!   (k < max(N, 2))
+  DevBuf newton_kernel_hat;         // NTT_{2N}((-1)^t / t!), scaled by 1/(2N)
+  DevBuf level_tables;              // per level: Vhat (2m) | Phat (2m)
+  std::vector<size_t> level_off;    // element offset of level l (m = 2^l) in level_tables
+};
+
+struct Srs {
+  DevBuf points;  // G1Affine[n]
+  size_t n = 0;
+  int device = 0;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  // workspaces
+  DevBuf scratch[8];
+  DevBuf msm_ws[10];
+  DevBuf prove_ws[12];  // resident trace / coefficient vectors of Twist/Shout::prove
+  DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
+  unsigned twiddle_log = 0;
+  std::vector<InterpPlan *> plans;  // indexed by log_n
+  ~Ctx();
+};
+
+// RAII device guard + lock
+struct CtxScope {
+  Ctx *c;
+  std::lock_guard<std::mutex> lk;
+  explicit CtxScope(Ctx *ctx) : c(ctx), lk(ctx->mu) { TNS_HIP(hipSetDevice(ctx->device)); }
+};
+
+inline unsigned grid_for(size_t work, unsigned block, unsigned max_blocks = 4096) {
+  size_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > max_blocks) g = max_blocks;
+  return (unsigned)g;
+}
+
+inline unsigned ilog2_exact(size_t n) {
+  unsigned l = 0;
+  while (((size_t)1 << l) < n) l++;
+  return l;
+}
+
+inline size_t next_pow2(size_t n) {  // Rust usize::next_power_of_two (0 -> 1)
+  size_t p = 1;
+  while (p < n) p <<= 1;
+  return p;
+}
+
+// ---- module entry points (device-resident pointers; all on ctx->stream) ----
+// mle.hip
+void mle_fold_dev(Ctx *c, const Fr *in, Fr *out, size_t half, const Fr &r);
+Fr mle_evaluate_dev(Ctx *c, const Fr *evals, unsigned nv, const Fr *point_host);
+struct SumcheckTerm {
+  Fr coeff;
+  int tab[3];
+};
+// Runs every round of SumCheck::prove over k device tables of 2^nv entries
+// (consumed: they are folded in place into workspace).  Transcript callback is
+// host-side.  Returns status; fills rounds (nv x 4), challenges, final values.
+struct HostTranscript;
+int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
+                       const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
+                       Fr *challenges, Fr *final_table_values, Fr *final_eval);
+
+// poly.hip
+// q[i] = c[i+1] + z q[i+1] (synthetic division by x - z); returns P(z).  q may be null.
+Fr synthetic_division_dev(Ctx *c, const Fr *coeffs, size_t n, const Fr &z, Fr *q);
+void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out);
+void to_mont_u64_dev(Ctx *c, const uint64_t *in, Fr *out, size_t n);
+void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
+
+// msm.hip
+G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n);
+
+// interp.hip
+void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs);
+
+// host-side helpers (transcript.cpp)
+struct HostTranscript {
+  std::vector<uint8_t> state;
+  void append_label(const char *s);
+  void append_bytes(const uint8_t *p, size_t n);
+  void append_fr(const Fr &x);
+  Fr challenge(const char *label);
+  Fr challenge_bytes(const uint8_t *label, size_t n);
+};
+Fr commitment_hash(const G1Affine &a);
+Fr host_fr_rand_chacha(const uint8_t seed[32], uint8_t *fs_seed_out /* nullable: next 32 bytes */);
+uint64_t siphash13_keys00(const uint8_t *msg, size_t n);
+void chacha20_block_host(const uint32_t key[8], uint64_t counter, uint32_t out[16]);
+// Lagrange interpolation of 4 points (0..3) for sum-check round polys (host, exact).
+void interpolate4_host(const Fr e[4], Fr out[4]);
+Fr horner_host(const Fr *c, int n, const Fr &z);
+
+}  // namespace tns

@@ -1,0 +1,301 @@
+// mle.hip -- multilinear-extension fold/evaluate and the fused sum-check round kernel.
+//
+// Reference semantics: MultilinearExtension::evaluate / partial_evaluate
+// (src/polynomials.rs:85-161) with variable j <-> index bit j (LSB first), and
+// SumCheck::prove (src/sumcheck.rs:56-110), whose round r sums the closure at
+// (r_0..r_{r-1}, X, suffix bits) for X in {0,1,2,3}.
+//
+// Instead of the reference's O(N * n) evaluate per hypercube point we keep each
+// MLE as a table and bind one variable per round:  T'[s] = T[2s] + r (T[2s+1] - T[2s]).
+// The round-k values at X are T_k[2s] + X (T_k[2s+1] - T_k[2s]).  One launch fuses
+// the fold by r_{k-1} with the round-k sums, so every round streams each table
+// once: read 32 B x (4 entries), write 32 B x 2 per output pair -- 48 B per input
+// entry, 96 B per entry over the whole chain (HBM-bound).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "common.hpp"
+
+namespace tns {
+
+constexpr int MAX_SC_TABLES = 4;
+constexpr int MAX_SC_TERMS = 16;
+
+struct ScTables {
+  const Fr *in[MAX_SC_TABLES];
+  Fr *out[MAX_SC_TABLES];
+};
+struct ScTerms {
+  Fr coeff[MAX_SC_TERMS];
+  int8_t tab[MAX_SC_TERMS][3];
+  int n;
+};
+
+// ---------------------------------------------------------------- wave/block reductions
+__device__ __forceinline__ Fr shfl_down_fr(const Fr &a, int d) {
+  Fr r;
+#pragma unroll
+  for (int i = 0; i < 8; i++) r.v[i] = __shfl_down(a.v[i], d, 64);
+  return r;
+}
+
+// Sum NV field elements across the block; thread 0 gets the result.  blockDim <= 1024.
+template <int NV>
+__device__ void block_sum_fr(Fr (&v)[NV], Fr *lds /* [NV][16] */) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
+      Fr o = shfl_down_fr(v[k], d);
+      if (lane + d < 64) v[k] = add(v[k], o);
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) lds[k * 16 + wid] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < NV; k++) {
+      Fr s = lds[k * 16];
+      for (int w = 1; w < nw; w++) s = add(s, lds[k * 16 + w]);
+      v[k] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- fold
+__global__ void __launch_bounds__(256) k_mle_fold(const Fr *__restrict__ in, Fr *__restrict__ out,
+                                                  size_t half, Fr r) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < half;
+       s += (size_t)gridDim.x * blockDim.x) {
+    Fr a = in[2 * s], b = in[2 * s + 1];
+    out[s] = add(a, mul(r, sub(b, a)));
+  }
+}
+
+void mle_fold_dev(Ctx *c, const Fr *in, Fr *out, size_t half, const Fr &r) {
+  k_mle_fold<<<grid_for(half, 256), 256, 0, c->stream>>>(in, out, half, r);
+  TNS_LAUNCH_CHECK();
+}
+
+// Evaluate by nv successive folds (ping-pong in scratch).  point_host: nv Fr.
+Fr mle_evaluate_dev(Ctx *c, const Fr *evals, unsigned nv, const Fr *point_host) {
+  if (nv == 0) {
+    Fr r;
+    TNS_HIP(hipMemcpyAsync(&r, evals, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipStreamSynchronize(c->stream));
+    return r;
+  }
+  size_t n = (size_t)1 << nv;
+  Fr *a = (Fr *)c->scratch[0].ensure(sizeof(Fr) * (n / 2));
+  Fr *b = (Fr *)c->scratch[1].ensure(sizeof(Fr) * (n / 4 > 0 ? n / 4 : 1));
+  const Fr *src = evals;
+  Fr *dst = a;
+  for (unsigned j = 0; j < nv; j++) {
+    size_t half = n >> (j + 1);
+    mle_fold_dev(c, src, dst, half, point_host[j]);
+    src = dst;
+    dst = (dst == a) ? b : a;
+  }
+  Fr r;
+  TNS_HIP(hipMemcpyAsync(&r, src, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  return r;
+}
+
+// ---------------------------------------------------------------- fused sum-check round
+// FOLD:   tables in[] have 4P entries; bind r into out[] (2P entries), then sum round values.
+// !FOLD:  tables in[] have 2P entries (first round), just sum.
+// Block partial sums (4 Fr: X = 0..3) -> partials[blockIdx.x * 4 + X].
+template <bool FOLD, bool TERMS>
+__global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms terms, size_t P, Fr r,
+                                                  Fr *__restrict__ partials) {
+  __shared__ Fr lds[4 * 16];
+  Fr acc[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P;
+       s += (size_t)gridDim.x * blockDim.x) {
+    Fr f0[MAX_SC_TABLES], f1[MAX_SC_TABLES];
+#pragma unroll
+    for (int i = 0; i < MAX_SC_TABLES; i++) {
+      if (i < k) {
+        if (FOLD) {
+          const Fr *p = t.in[i] + 4 * s;
+          Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+          f0[i] = add(x0, mul(r, sub(x1, x0)));
+          f1[i] = add(x2, mul(r, sub(x3, x2)));
+          t.out[i][2 * s] = f0[i];
+          t.out[i][2 * s + 1] = f1[i];
+        } else {
+          f0[i] = t.in[i][2 * s];
+          f1[i] = t.in[i][2 * s + 1];
+        }
+      }
+    }
+    if (TERMS) {
+      // values at X = 0,1,2,3: f0, f1, f1 + d, f1 + 2d
+      Fr d[MAX_SC_TABLES];
+#pragma unroll
+      for (int i = 0; i < MAX_SC_TABLES; i++)
+        if (i < k) d[i] = sub(f1[i], f0[i]);
+      for (int x = 0; x < 4; x++) {
+        Fr vx[MAX_SC_TABLES];
+#pragma unroll
+        for (int i = 0; i < MAX_SC_TABLES; i++) {
+          if (i < k) {
+            if (x == 0) vx[i] = f0[i];
+            else if (x == 1) vx[i] = f1[i];
+            else if (x == 2) vx[i] = add(f1[i], d[i]);
+            else vx[i] = add(add(f1[i], d[i]), d[i]);
+          }
+        }
+        Fr sum = Fr::zero();
+        for (int tt = 0; tt < terms.n; tt++) {
+          Fr p = terms.coeff[tt];
+#pragma unroll
+          for (int j = 0; j < 3; j++) {
+            int ix = terms.tab[tt][j];
+            if (ix >= 0) {
+              Fr v = vx[0];
+#pragma unroll
+              for (int q = 1; q < MAX_SC_TABLES; q++)
+                if (ix == q) v = vx[q];
+              p = mul(p, v);
+            }
+          }
+          sum = add(sum, p);
+        }
+        acc[x] = add(acc[x], sum);
+      }
+    }
+  }
+  if (TERMS) {
+    block_sum_fr<4>(acc, lds);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int x = 0; x < 4; x++) partials[blockIdx.x * 4 + x] = acc[x];
+    }
+  }
+}
+
+// Sum nb blocks' 4-vectors -> out[0..3]
+__global__ void __launch_bounds__(256) k_sum_partials4(const Fr *__restrict__ partials, int nb,
+                                                       Fr *__restrict__ out) {
+  __shared__ Fr lds[4 * 16];
+  Fr acc[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    for (int x = 0; x < 4; x++) acc[x] = add(acc[x], partials[b * 4 + x]);
+  block_sum_fr<4>(acc, lds);
+  if (threadIdx.x == 0)
+    for (int x = 0; x < 4; x++) out[x] = acc[x];
+}
+
+static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n_terms) {
+  Fr s = Fr::zero();
+  for (int t = 0; t < n_terms; t++) {
+    Fr p = terms[t].coeff;
+    for (int j = 0; j < 3; j++)
+      if (terms[t].tab[j] >= 0) p = mul(p, vals[terms[t].tab[j]]);
+    s = add(s, p);
+  }
+  return s;
+}
+
+// SumCheck::prove (src/sumcheck.rs:56-110) for an MLE composition.
+// tables: k device arrays of 2^nv Fr (overwritten).  Host transcript drives challenges.
+int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
+                       const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
+                       Fr *challenges, Fr *final_vals, Fr *final_eval) {
+  if (k < 0 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
+  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
+  ScTerms st{};
+  st.n = n_terms;
+  for (int t = 0; t < n_terms; t++) {
+    st.coeff[t] = terms[t].coeff;
+    for (int j = 0; j < 3; j++) {
+      int ix = terms[t].tab[j];
+      if (ix >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
+      st.tab[t][j] = (int8_t)ix;
+    }
+  }
+  const bool has_terms = n_terms > 0;
+  const size_t n = (size_t)1 << nv;
+  // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)).
+  Fr *bufB[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
+  const int nblk = (int)grid_for(n / 2 + 1, 256, 2048);
+  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * 4 * (size_t)nblk);
+  Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
+
+  Fr cur = claimed;
+  Fr *src[MAX_SC_TABLES], *dst[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    src[i] = tables[i];
+    dst[i] = bufB[i];
+  }
+  Fr r_prev = Fr::zero();
+  char lab[64];
+  for (unsigned rnd = 0; rnd < nv; rnd++) {
+    const size_t P = n >> (rnd + 1);  // output pairs of this round
+    ScTables tt{};
+    for (int i = 0; i < k; i++) {
+      tt.in[i] = src[i];
+      tt.out[i] = dst[i];
+    }
+    const unsigned g = grid_for(P, 256, 2048);
+    if (rnd == 0) {
+      if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+    } else {
+      if (has_terms)
+        k_sc_round<true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+      else
+        k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+      // src now holds the freshly folded 2P-entry tables; the caller's tables
+      // become the next destination (they are consumed).
+      for (int i = 0; i < k; i++) std::swap(src[i], dst[i]);
+    }
+    TNS_LAUNCH_CHECK();
+    Fr e[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
+    if (has_terms) {
+      k_sum_partials4<<<1, 256, 0, c->stream>>>(partials, (int)g, sums_dev);
+      TNS_LAUNCH_CHECK();
+      TNS_HIP(hipMemcpyAsync(e, sums_dev, sizeof e, hipMemcpyDeviceToHost, c->stream));
+      TNS_HIP(hipStreamSynchronize(c->stream));
+    }
+    Fr coeffs[4];
+    interpolate4_host(e, coeffs);  // lagrange_interpolate of 4 points (src/sumcheck.rs:201-206)
+    Fr g0 = horner_host(coeffs, 4, Fr::zero());
+    Fr g1 = horner_host(coeffs, 4, Fr::one());
+    if (add(g0, g1) != cur) {  // src/sumcheck.rs:80-84
+      snprintf(lab, sizeof lab, "Round %u consistency check failed", rnd);
+      throw Error(TNS_ERR_SUMCHECK, lab);
+    }
+    for (int x = 0; x < 4; x++) rounds[4 * rnd + x] = coeffs[x];
+    snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd);  // src/sumcheck.rs:90-96
+    tr.append_label(lab);
+    for (int x = 0; x < 4; x++) tr.append_fr(coeffs[x]);
+    snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
+    Fr ch = tr.challenge(lab);
+    if (challenges) challenges[rnd] = ch;
+    cur = horner_host(coeffs, 4, ch);
+    r_prev = ch;
+  }
+  // bind the last variable: final MLE values at (r_0..r_{nv-1})
+  Fr vals[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    if (nv == 0) {
+      TNS_HIP(hipMemcpyAsync(&vals[i], src[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+    } else {
+      mle_fold_dev(c, src[i], dst[i], 1, r_prev);
+      TNS_HIP(hipMemcpyAsync(&vals[i], dst[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+    }
+  }
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < k; i++) final_vals[i] = vals[i];
+  *final_eval = eval_composition_host(vals, terms, n_terms);  // polynomial(&fixed_variables), :104
+  return TNS_OK;
+}
+
+}  // namespace tns

@@ -1,0 +1,291 @@
+// msm.hip -- BN254 G1 multi-scalar multiplication (Pippenger, signed windows).
+//
+// Replaces KZGCommitment::commit's per-term scalar multiplications
+// (src/commitments.rs:173-177): C = sum_i c_i * g1_powers[i].  The group element
+// is unique, so any correct algorithm reproduces it exactly.
+//
+// Pipeline (all on one stream):
+//  1. k_digits: scalar -> canonical -> W signed c-bit digits; key = (window, |d|-1),
+//     value = point index | sign<<31; zero digits get a sentinel key.
+//  2. rocPRIM/hipCUB radix sort of the W*n (key, value) pairs by key.
+//  3. k_bucket_bounds: [start, end) of every bucket in the sorted order.
+//  4. k_accumulate: load-balanced -- each thread owns K consecutive sorted entries
+//     and XYZZ-madds the (possibly negated) affine points run by run; runs that
+//     cross a chunk boundary leave a head/tail partial.
+//  5. k_bucket_fixup: buckets spanning chunks = tail + heads; empty -> identity.
+//  6. k_bucket_reduce + k_window_sum: S_w = sum_j (j+1) B_{w,j} via per-group
+//     running sums, then a block tree per window.
+//  7. host: sum_w 2^(c w) S_w (Horner, W*c doublings).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+#include "common.hpp"
+
+namespace tns {
+
+constexpr int ACC_K = 32;      // sorted entries per accumulation thread
+constexpr int RED_L = 16;      // buckets per reduction thread
+
+struct MsmPlan {
+  int c, W, wbits;
+  uint32_t sentinel;
+  int end_bit;
+  size_t nb;  // W * 2^(c-1)
+};
+
+static MsmPlan make_plan(size_t n) {
+  MsmPlan p;
+  int lg = 0;
+  while (((size_t)1 << lg) < n) lg++;
+  p.c = lg - 3;
+  if (p.c < 4) p.c = 4;
+  if (p.c > 16) p.c = 16;
+  p.W = (254 + p.c - 1) / p.c;
+  // the top window must not produce a carry: its raw value < 2^(254 - c(W-1)) must be <= 2^(c-1)
+  if (254 - p.c * (p.W - 1) > p.c - 1) p.W++;
+  p.wbits = 0;
+  while ((1 << p.wbits) < p.W) p.wbits++;
+  p.end_bit = p.wbits + (p.c - 1) + 1;
+  p.sentinel = 1u << (p.wbits + p.c - 1);
+  p.nb = (size_t)p.W << (p.c - 1);
+  return p;
+}
+
+__global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, size_t n, int c, int W,
+                                                uint32_t sentinel, uint32_t *__restrict__ keys,
+                                                uint32_t *__restrict__ vals) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    Fr k = from_mont(scalars[i]);
+    uint32_t carry = 0;
+    const uint32_t half = 1u << (c - 1);
+    for (int w = 0; w < W; w++) {
+      int bit = w * c;
+      int limb = bit >> 5, sh = bit & 31;
+      uint64_t lo = limb < 8 ? k.v[limb] : 0;
+      uint64_t hi = limb + 1 < 8 ? k.v[limb + 1] : 0;
+      uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1u << c) - 1));
+      uint32_t val = raw + carry;
+      uint32_t key, neg = 0, mag;
+      if (val > half) {
+        mag = (1u << c) - val;
+        neg = 1;
+        carry = 1;
+      } else {
+        mag = val;
+        carry = 0;
+      }
+      key = mag ? (((uint32_t)w << (c - 1)) | (mag - 1)) : sentinel;
+      keys[(size_t)w * n + i] = key;
+      vals[(size_t)w * n + i] = (uint32_t)i | (neg << 31);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_bucket_bounds(const uint32_t *__restrict__ keys, size_t total,
+                                                       uint32_t sentinel, uint32_t *__restrict__ start,
+                                                       uint32_t *__restrict__ end,
+                                                       uint32_t *__restrict__ valid) {
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < total;
+       p += (size_t)gridDim.x * blockDim.x) {
+    uint32_t k = keys[p];
+    if (k == sentinel) continue;
+    if (p == 0 || keys[p - 1] != k) start[k] = (uint32_t)p;
+    uint32_t nx = (p + 1 < total) ? keys[p + 1] : sentinel;
+    if (nx != k) end[k] = (uint32_t)(p + 1);
+    if (nx == sentinel) *valid = (uint32_t)(p + 1);
+  }
+}
+
+struct HeadTail {
+  G1Xyzz head, tail;
+};
+
+__device__ __forceinline__ G1Affine load_signed_point(const G1Affine *__restrict__ pts, uint32_t v) {
+  G1Affine p = pts[v & 0x7fffffffu];
+  if (v >> 31) p.y = neg(p.y);
+  return p;
+}
+
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ keys,
+                                                    const uint32_t *__restrict__ vals,
+                                                    const uint32_t *__restrict__ valid_p,
+                                                    const uint32_t *__restrict__ start,
+                                                    const uint32_t *__restrict__ end,
+                                                    const G1Affine *__restrict__ pts,
+                                                    G1Xyzz *__restrict__ buckets,
+                                                    HeadTail *__restrict__ ht, size_t nchunks) {
+  const size_t valid = *valid_p;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const size_t a = t * ACC_K;
+    if (a >= valid) continue;
+    size_t b = a + ACC_K;
+    if (b > valid) b = valid;
+    uint32_t cur = keys[a];
+    G1Xyzz acc = G1Xyzz::inf();
+    for (size_t p = a;; p++) {
+      uint32_t k = (p < b) ? keys[p] : 0xffffffffu;
+      if (k != cur) {
+        // flush run of bucket `cur`
+        uint32_t s = start[cur], e = end[cur];
+        if (s < a) ht[t].head = acc;
+        else if (e > b) ht[t].tail = acc;
+        else buckets[cur] = acc;
+        if (p >= b) break;
+        cur = k;
+        acc = G1Xyzz::inf();
+      }
+      acc = xyzz_madd(acc, load_signed_point(pts, vals[p]));
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
+                                                      const uint32_t *__restrict__ end,
+                                                      const HeadTail *__restrict__ ht,
+                                                      G1Xyzz *__restrict__ buckets, size_t nb) {
+  for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb;
+       bk += (size_t)gridDim.x * blockDim.x) {
+    uint32_t s = start[bk], e = end[bk];
+    if (s == e) {
+      buckets[bk] = G1Xyzz::inf();
+      continue;
+    }
+    size_t tf = s / ACC_K, tl = (e - 1) / ACC_K;
+    if (tf == tl) continue;
+    G1Xyzz acc = ht[tf].tail;
+    for (size_t t = tf + 1; t <= tl; t++) acc = xyzz_add(acc, ht[t].head);
+    buckets[bk] = acc;
+  }
+}
+
+// per (window, group): sum_{j in group} (j+1) B_j
+__global__ void __launch_bounds__(256) k_bucket_reduce(const G1Xyzz *__restrict__ buckets, int W,
+                                                       int half_buckets, G1Xyzz *__restrict__ out) {
+  const int groups = half_buckets / RED_L;
+  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)W * groups;
+       id += (size_t)gridDim.x * blockDim.x) {
+    int w = (int)(id / groups), g = (int)(id % groups);
+    const G1Xyzz *B = buckets + (size_t)w * half_buckets;
+    int a = g * RED_L;
+    G1Xyzz run = G1Xyzz::inf(), acc = G1Xyzz::inf();
+    for (int j = a + RED_L - 1; j >= a; j--) {
+      run = xyzz_add(run, B[j]);
+      acc = xyzz_add(acc, run);
+    }
+    if (a) acc = xyzz_add(acc, xyzz_mul_small(run, (uint64_t)a));
+    out[id] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_window_sum(const G1Xyzz *__restrict__ parts, int groups,
+                                                    G1Xyzz *__restrict__ out) {
+  __shared__ G1Xyzz lds[256];
+  const int w = blockIdx.x;
+  G1Xyzz acc = G1Xyzz::inf();
+  for (int g = threadIdx.x; g < groups; g += blockDim.x) acc = xyzz_add(acc, parts[(size_t)w * groups + g]);
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) lds[threadIdx.x] = xyzz_add(lds[threadIdx.x], lds[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[w] = lds[0];
+}
+
+// Naive path for tiny inputs: one thread per point, double-and-add, then a tree.
+__global__ void __launch_bounds__(64) k_msm_tiny(const G1Affine *__restrict__ pts,
+                                                 const Fr *__restrict__ scalars, int n,
+                                                 G1Xyzz *__restrict__ out) {
+  __shared__ G1Xyzz lds[64];
+  G1Xyzz acc = G1Xyzz::inf();
+  for (int i = threadIdx.x; i < n; i += 64) {
+    Fr k = from_mont(scalars[i]);
+    G1Xyzz r = G1Xyzz::inf();
+    for (int b = 253; b >= 0; b--) {
+      r = xyzz_dbl(r);
+      if ((k.v[b >> 5] >> (b & 31)) & 1) r = xyzz_madd(r, pts[i]);
+    }
+    acc = xyzz_add(acc, r);
+  }
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = 32; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) lds[threadIdx.x] = xyzz_add(lds[threadIdx.x], lds[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = lds[0];
+}
+
+G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
+  if (n == 0) return G1Xyzz::inf();
+  hipStream_t st = ctx->stream;
+  if (n <= 64) {
+    G1Xyzz *d = (G1Xyzz *)ctx->msm_ws[0].ensure(sizeof(G1Xyzz));
+    k_msm_tiny<<<1, 64, 0, st>>>(points, scalars, (int)n, d);
+    TNS_LAUNCH_CHECK();
+    G1Xyzz h;
+    TNS_HIP(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
+    TNS_HIP(hipStreamSynchronize(st));
+    return h;
+  }
+  if (n >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM larger than 2^31 points");
+  const MsmPlan P = make_plan(n);
+  const size_t total = (size_t)P.W * n;
+  if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
+  const int half = 1 << (P.c - 1);
+
+  uint32_t *keys = (uint32_t *)ctx->msm_ws[0].ensure(sizeof(uint32_t) * total);
+  uint32_t *vals = (uint32_t *)ctx->msm_ws[1].ensure(sizeof(uint32_t) * total);
+  uint32_t *keys2 = (uint32_t *)ctx->msm_ws[2].ensure(sizeof(uint32_t) * total);
+  uint32_t *vals2 = (uint32_t *)ctx->msm_ws[3].ensure(sizeof(uint32_t) * total);
+  uint32_t *bounds = (uint32_t *)ctx->msm_ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
+  uint32_t *bstart = bounds, *bend = bounds + P.nb, *valid = bounds + 2 * P.nb;
+  G1Xyzz *buckets = (G1Xyzz *)ctx->msm_ws[5].ensure(sizeof(G1Xyzz) * P.nb);
+  const size_t nchunks = (total + ACC_K - 1) / ACC_K;
+  HeadTail *ht = (HeadTail *)ctx->msm_ws[6].ensure(sizeof(HeadTail) * nchunks);
+  const int groups = half / RED_L > 0 ? half / RED_L : 1;
+  G1Xyzz *parts = (G1Xyzz *)ctx->msm_ws[7].ensure(sizeof(G1Xyzz) * (size_t)P.W * groups);
+  G1Xyzz *wsum = (G1Xyzz *)ctx->msm_ws[8].ensure(sizeof(G1Xyzz) * P.W);
+
+  k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, keys, vals);
+  TNS_LAUNCH_CHECK();
+
+  size_t temp_bytes = 0;
+  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total,
+                                             0, P.end_bit, st));
+  void *temp = ctx->msm_ws[9].ensure(temp_bytes);
+  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
+                                             P.end_bit, st));
+
+  TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
+  k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
+  TNS_LAUNCH_CHECK();
+  k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
+                                                                 points, buckets, ht, nchunks);
+  TNS_LAUNCH_CHECK();
+  k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, buckets, P.nb);
+  TNS_LAUNCH_CHECK();
+  if (half >= RED_L) {
+    k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, parts);
+    TNS_LAUNCH_CHECK();
+    k_window_sum<<<P.W, 256, 0, st>>>(parts, groups, wsum);
+  } else {
+    throw Error(TNS_ERR_COMMITMENT, "MSM window too small");
+  }
+  TNS_LAUNCH_CHECK();
+  std::vector<G1Xyzz> S(P.W);
+  TNS_HIP(hipMemcpyAsync(S.data(), wsum, sizeof(G1Xyzz) * P.W, hipMemcpyDeviceToHost, st));
+  TNS_HIP(hipStreamSynchronize(st));
+  G1Xyzz acc = S[P.W - 1];
+  for (int w = P.W - 2; w >= 0; w--) {
+    for (int k = 0; k < P.c; k++) acc = xyzz_dbl(acc);
+    acc = xyzz_add(acc, S[w]);
+  }
+  return acc;
+}
+
+}  // namespace tns

@@ -1,0 +1,674 @@
+"""twist_and_shout -- MI355X-native prover hot path with the reference crate's API.
+
+Host-side mirror of the Rust crate ``twist-and-shout`` (/root/reference/src/lib.rs:41-56)
+over the C ABI of ``libtns.so`` (include/tns.h).  Names, argument meaning and error
+behaviour follow the reference:
+
+* ``setup_params(log_size)``                       -- src/utils.rs:79-131
+* ``MemoryTrace`` / ``Twist.prove``                 -- src/twist.rs:24-252
+* ``LookupTable`` / ``Shout.prove``                 -- src/shout.rs:26-222
+* ``KZGCommitment.commit/open``, ``KZGCommitmentValue.hash`` -- src/commitments.rs:73-199
+* ``MultilinearExtension``                          -- src/polynomials.rs:18-196
+* ``SumCheck.prove``                                -- src/sumcheck.rs:56-110
+* ``Transcript``                                    -- src/utils.rs:134-204
+* ``poly_utils.lagrange_interpolate`` on nodes 0..n-1 -- src/polynomials.rs:301-352
+
+Field elements are Python ints (canonical representatives mod r); bulk data is
+passed to the device as uint64 (n, 4) Montgomery arrays (arkworks' memory layout).
+Errors raise ``TwistAndShoutError`` subclasses named after the Rust enum variants
+(src/lib.rs:59-78).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+R_MOD = 0x30644E72E131A029B85045B68181585D2833E84879B9709143E1F593F0000001
+P_MOD = 0x30644E72E131A029B85045B68181585D97816A916871CA8D3C208C16D87CFD47
+_MONT_R = 1 << 256
+_MASK64 = (1 << 64) - 1
+
+FieldElement = int
+G1Affine = Optional[Tuple[int, int]]  # None = identity
+
+
+# ----------------------------------------------------------------------------- errors
+class TwistAndShoutError(Exception):
+    """src/lib.rs:59-78"""
+
+
+class InvalidParameters(TwistAndShoutError):
+    pass
+
+
+class ProofGeneration(TwistAndShoutError):
+    pass
+
+
+class ProofVerification(TwistAndShoutError):
+    pass
+
+
+class CommitmentError(TwistAndShoutError):
+    pass
+
+
+class PolynomialError(TwistAndShoutError):
+    pass
+
+
+class SumCheckError(TwistAndShoutError):
+    pass
+
+
+class DeviceError(TwistAndShoutError):
+    pass
+
+
+_ERRORS = {1: InvalidParameters, 2: ProofGeneration, 3: ProofVerification, 4: CommitmentError,
+           5: PolynomialError, 6: SumCheckError}
+
+
+def _check(status: int):
+    if status != 0:
+        raise _ERRORS.get(status, DeviceError)(f"[{N.STATUS_NAMES.get(status, status)}] {N.last_error()}")
+
+
+# ----------------------------------------------------------------------------- conversions
+def to_mont(values: Sequence[int], mod: int = R_MOD) -> np.ndarray:
+    out = np.empty((len(values), 4), dtype=np.uint64)
+    for i, v in enumerate(values):
+        m = (int(v) % mod) * _MONT_R % mod
+        out[i] = [(m >> 0) & _MASK64, (m >> 64) & _MASK64, (m >> 128) & _MASK64, (m >> 192) & _MASK64]
+    return out
+
+
+def _limbs_to_int(row) -> int:
+    return int(row[0]) | int(row[1]) << 64 | int(row[2]) << 128 | int(row[3]) << 192
+
+
+def from_mont(arr: np.ndarray, mod: int = R_MOD) -> List[int]:
+    arr = np.ascontiguousarray(arr, dtype=np.uint64).reshape(-1, 4)
+    canon = np.empty_like(arr)
+    if len(arr):
+        (N.load().tns_fr_to_canonical if mod == R_MOD else N.load().tns_fq_to_canonical)(
+            N.p64(arr), len(arr), N.p64(canon))
+    return [_limbs_to_int(r) for r in canon]
+
+
+def fr_from_u64_array(vals: np.ndarray) -> np.ndarray:
+    """Bulk Fr::from(u64) into Montgomery limbs (multi-threaded in libtns)."""
+    v = np.ascontiguousarray(vals, dtype=np.uint64)
+    out = np.empty((len(v), 4), dtype=np.uint64)
+    if len(v):
+        N.load().tns_fr_from_u64(N.p64(v), len(v), N.p64(out))
+    return out
+
+
+def _g1_from_proj(limbs) -> G1Affine:
+    a = np.ascontiguousarray(np.asarray(limbs, dtype=np.uint64).reshape(3, 4))
+    if not a[2].any():
+        return None
+    x, y = from_mont(a[:2], P_MOD)
+    return (x, y)  # outputs are normalised with Z = 1
+
+
+# ----------------------------------------------------------------------------- device context
+class Context:
+    """One libtns context (HIP stream + workspaces) per device and process."""
+
+    _lock = threading.Lock()
+    _by_device: dict = {}
+
+    def __init__(self, device: int = 0):
+        lib = N.load()
+        h = C.c_void_p()
+        _check(lib.tns_ctx_create(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    @classmethod
+    def get(cls, device: int = 0) -> "Context":
+        with cls._lock:
+            if device not in cls._by_device:
+                cls._by_device[device] = Context(device)
+            return cls._by_device[device]
+
+    def timing(self):
+        out = (C.c_double * 6)()
+        N.load().tns_last_prove_timing(self.handle, out)
+        return dict(zip(["h2d", "interpolate", "commit", "sumcheck", "open", "total"], list(out)))
+
+
+def device_count() -> int:
+    return N.load().tns_device_count()
+
+
+# ----------------------------------------------------------------------------- params
+class Srs:
+    """Device-resident CommitmentParams.g1_powers."""
+
+    def __init__(self, ctx: Context, handle: C.c_void_p):
+        self.ctx = ctx
+        self.handle = handle
+
+    def __len__(self):
+        return N.load().tns_srs_len(self.handle)
+
+    def download(self, n: Optional[int] = None) -> np.ndarray:
+        n = len(self) if n is None else n
+        out = np.zeros((n, 8), dtype=np.uint64)
+        _check(N.load().tns_srs_download(self.ctx.handle, self.handle, N.p64(out), n))
+        return out
+
+    def __del__(self):
+        try:
+            N.load().tns_srs_destroy(self.handle)
+        except Exception:
+            pass
+
+
+@dataclass
+class CommitmentParams:
+    """src/utils.rs:53-63 (g2_generator is verifier-side and not materialised here)."""
+    srs: Srs
+    tau: Optional[int]
+
+    @property
+    def g1_powers(self) -> List[G1Affine]:
+        limbs = self.srs.download()
+        xs = from_mont(limbs[:, :4], P_MOD)
+        ys = from_mont(limbs[:, 4:], P_MOD)
+        return [None if (x == 0 and y == 0) else (x, y) for x, y in zip(xs, ys)]
+
+    @classmethod
+    def from_g1_powers(cls, g1_powers: Sequence[G1Affine], device: int = 0, tau=None) -> "CommitmentParams":
+        ctx = Context.get(device)
+        flat = []
+        for P in g1_powers:
+            flat.append((0, 0) if P is None else P)
+        arr = np.zeros((len(flat), 8), dtype=np.uint64)
+        if flat:
+            arr[:, :4] = to_mont([p[0] for p in flat], P_MOD)
+            arr[:, 4:] = to_mont([p[1] for p in flat], P_MOD)
+            for i, P in enumerate(g1_powers):
+                if P is None:
+                    arr[i] = 0
+        h = C.c_void_p()
+        _check(N.load().tns_srs_upload(ctx.handle, N.p64(arr), len(arr), C.byref(h)))
+        return cls(Srs(ctx, h), tau)
+
+
+@dataclass
+class ProverParams:
+    """src/utils.rs:21-34"""
+    log_size: int
+    max_operations: int
+    commitment_params: CommitmentParams
+    fiat_shamir_seed: bytes
+    _raw: N.TnsParams = field(repr=False, default=None)
+
+    def raw(self) -> N.TnsParams:
+        if self._raw is None:
+            r = N.TnsParams()
+            r.log_size = self.log_size
+            r.max_operations = self.max_operations
+            r.num_powers = len(self.commitment_params.srs)
+            r.fiat_shamir_seed = (C.c_uint8 * 32)(*self.fiat_shamir_seed)
+            self._raw = r
+        return self._raw
+
+
+@dataclass
+class VerifierParams:
+    """src/utils.rs:37-50 (commitment_vk / G2 elements: verifier side, out of scope)."""
+    log_size: int
+    max_operations: int
+    fiat_shamir_seed: bytes
+
+
+def setup_params(log_size: int, device: int = 0) -> Tuple[ProverParams, VerifierParams]:
+    """src/utils.rs:79-131 -- tau and the FS seed from ChaCha20Rng([42;32]); SRS on the GPU."""
+    ctx = Context.get(device)
+    raw = N.TnsParams()
+    h = C.c_void_p()
+    _check(N.load().tns_setup_params(ctx.handle, log_size, C.byref(raw), C.byref(h)))
+    tau = from_mont(np.array(list(raw.tau), dtype=np.uint64))[0]
+    seed = bytes(raw.fiat_shamir_seed)
+    cp = CommitmentParams(Srs(ctx, h), tau)
+    pp = ProverParams(int(raw.log_size), int(raw.max_operations), cp, seed, raw)
+    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed)
+
+
+# ----------------------------------------------------------------------------- transcript
+class Transcript:
+    """src/utils.rs:134-204 (host side; the same code drives the device prover)."""
+
+    def __init__(self, seed: bytes = bytes(32)):
+        self._h = N.load().tns_transcript_new((C.c_uint8 * 32)(*seed))
+
+    def __del__(self):
+        try:
+            N.load().tns_transcript_free(self._h)
+        except Exception:
+            pass
+
+    @staticmethod
+    def _lab(label: bytes):
+        return (C.c_uint8 * max(1, len(label))).from_buffer_copy(label or b"\0"), len(label)
+
+    def append_field_element(self, label: bytes, x: int):
+        lab, n = self._lab(label)
+        a = to_mont([x])
+        N.load().tns_transcript_append_field_element(self._h, lab, n, N.p64(a))
+
+    def append_field_elements(self, label: bytes, xs: Sequence[int]):
+        lab, n = self._lab(label)
+        a = to_mont(list(xs)) if len(xs) else np.zeros((1, 4), dtype=np.uint64)
+        N.load().tns_transcript_append_field_elements(self._h, lab, n, N.p64(a), len(xs))
+
+    def challenge_field_element(self, label: bytes) -> int:
+        lab, n = self._lab(label)
+        out = np.zeros(4, dtype=np.uint64)
+        N.load().tns_transcript_challenge_field_element(self._h, lab, n, N.p64(out))
+        return from_mont(out)[0]
+
+    def challenge_field_elements(self, label: bytes, count: int) -> List[int]:
+        return [self.challenge_field_element(label + b"_" + str(i).encode()) for i in range(count)]
+
+
+# ----------------------------------------------------------------------------- KZG
+@dataclass
+class KZGCommitmentValue:
+    """src/commitments.rs:67-85"""
+    commitment: G1Affine
+    _proj: np.ndarray = field(repr=False, default=None, compare=False)
+
+    def hash(self) -> int:
+        out = np.zeros(4, dtype=np.uint64)
+        proj = self._proj if self._proj is not None else _affine_to_proj(self.commitment)
+        _check(N.load().tns_commitment_hash(N.p64(np.ascontiguousarray(proj)), N.p64(out)))
+        return from_mont(out)[0]
+
+
+@dataclass
+class KZGProof:
+    """src/commitments.rs:89-91"""
+    proof: G1Affine
+
+
+def _affine_to_proj(P: G1Affine) -> np.ndarray:
+    if P is None:
+        one = to_mont([1], P_MOD)[0]
+        return np.concatenate([one, one, np.zeros(4, dtype=np.uint64)])
+    return np.concatenate([to_mont([P[0]], P_MOD)[0], to_mont([P[1]], P_MOD)[0], to_mont([1], P_MOD)[0]])
+
+
+def _as_mont(poly) -> np.ndarray:
+    if isinstance(poly, np.ndarray):
+        return np.ascontiguousarray(poly, dtype=np.uint64).reshape(-1, 4)
+    return to_mont(list(poly)) if len(poly) else np.zeros((0, 4), dtype=np.uint64)
+
+
+def _nonempty(a: np.ndarray) -> np.ndarray:
+    return a if len(a) else np.zeros((1, 4), dtype=np.uint64)
+
+
+class KZGCommitment:
+    """``impl CommitmentScheme for KZGCommitment`` (src/commitments.rs:156-302), prover half."""
+
+    @staticmethod
+    def commit(params: CommitmentParams, polynomial) -> KZGCommitmentValue:
+        c = _as_mont(polynomial)
+        out = np.zeros(12, dtype=np.uint64)
+        _check(N.load().tns_kzg_commit(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(c)), len(c),
+                                       N.p64(out)))
+        return KZGCommitmentValue(_g1_from_proj(out), out)
+
+    @staticmethod
+    def open(params: CommitmentParams, polynomial, point: int) -> Tuple[int, KZGProof]:
+        c = _as_mont(polynomial)
+        z = to_mont([point])[0]
+        v = np.zeros(4, dtype=np.uint64)
+        pi = np.zeros(12, dtype=np.uint64)
+        _check(N.load().tns_kzg_open(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(c)), len(c),
+                                     N.p64(z), N.p64(v), N.p64(pi)))
+        return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
+
+
+def msm(params: CommitmentParams, scalars) -> G1Affine:
+    """Raw G1 MSM over the first len(scalars) SRS points (the commit kernel)."""
+    c = _as_mont(scalars)
+    out = np.zeros(12, dtype=np.uint64)
+    _check(N.load().tns_msm(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(c)), len(c), N.p64(out)))
+    return _g1_from_proj(out)
+
+
+# ----------------------------------------------------------------------------- polynomials
+class poly_utils:  # noqa: N801  (mirrors the Rust module name)
+    @staticmethod
+    def interpolate_consecutive(values, device: int = 0) -> np.ndarray:
+        """lagrange_interpolate over nodes (0..n-1); Montgomery array in, Montgomery array out."""
+        y = _as_mont(values)
+        out = np.zeros_like(y)
+        if len(y):
+            _check(N.load().tns_interpolate_consecutive(Context.get(device).handle, N.p64(y), len(y), N.p64(out)))
+        return out
+
+    @staticmethod
+    def lagrange_interpolate(points: Sequence[Tuple[int, int]], device: int = 0) -> List[int]:
+        """src/polynomials.rs:301-352 for the node set the prover uses (x_i = i, n a power of two)."""
+        n = len(points)
+        if n == 0:
+            return []
+        if any(int(x) % R_MOD != i for i, (x, _) in enumerate(points)) or (n & (n - 1)):
+            raise PolynomialError("device interpolation supports the nodes 0..n-1 with n a power of two")
+        return from_mont(poly_utils.interpolate_consecutive([y for _, y in points], device))
+
+    @staticmethod
+    def evaluate_polynomial(coeffs: Sequence[int], point: int) -> int:
+        """src/polynomials.rs:355-357 (Horner; host)."""
+        acc = 0
+        for c in reversed(coeffs):
+            acc = (acc * point + c) % R_MOD
+        return acc
+
+
+class MultilinearExtension:
+    """src/polynomials.rs:18-196 -- evaluate / partial_evaluate run on the GPU (fold kernels)."""
+
+    def __init__(self, num_vars: int, evaluations: Sequence[int]):
+        self.num_vars = num_vars
+        self.evaluations = [int(e) % R_MOD for e in evaluations]
+
+    @classmethod
+    def from_evaluations(cls, evaluations):  # :28-37
+        n = len(evaluations)
+        nv = max(n.bit_length() - 1, 0)
+        if (1 << nv) != n:
+            raise AssertionError("Evaluation vector length must be a power of 2")
+        return cls(nv, evaluations)
+
+    @classmethod
+    def from_evaluations_vec(cls, num_vars: int, evaluations):  # :40-50
+        size = 1 << num_vars
+        e = list(evaluations)[:size]
+        return cls(num_vars, e + [0] * (size - len(e)))
+
+    @classmethod
+    def from_sparse(cls, num_vars: int, entries):  # :54-67
+        ev = [0] * (1 << num_vars)
+        for i, v in entries:
+            if i >= len(ev):
+                raise AssertionError(f"Index {i} out of bounds for size {len(ev)}")
+            ev[i] = v
+        return cls(num_vars, ev)
+
+    @classmethod
+    def one_hot(cls, num_vars: int, index: int):  # :71-82
+        if index >= (1 << num_vars):
+            raise AssertionError("Index out of bounds")
+        ev = [0] * (1 << num_vars)
+        ev[index] = 1
+        return cls(num_vars, ev)
+
+    def evaluate(self, point: Sequence[int], device: int = 0) -> int:  # :85-103
+        if len(point) != self.num_vars:
+            raise AssertionError("Point dimension must match number of variables")
+        ev = to_mont(self.evaluations)
+        pt = _nonempty(to_mont(list(point)))
+        out = np.zeros(4, dtype=np.uint64)
+        _check(N.load().tns_mle_evaluate(Context.get(device).handle, N.p64(ev), self.num_vars, N.p64(pt),
+                                         N.p64(out)))
+        return from_mont(out)[0]
+
+    def partial_evaluate(self, fixed: Sequence[int], device: int = 0) -> "MultilinearExtension":  # :126-161
+        k = len(fixed)
+        if k > self.num_vars:
+            raise AssertionError("Cannot fix more variables than available")
+        if k == 0:
+            return MultilinearExtension(self.num_vars, list(self.evaluations))
+        ev = to_mont(self.evaluations)
+        fx = to_mont(list(fixed))
+        out = np.zeros((1 << (self.num_vars - k), 4), dtype=np.uint64)
+        _check(N.load().tns_mle_partial_evaluate(Context.get(device).handle, N.p64(ev), self.num_vars,
+                                                 N.p64(fx), k, N.p64(out)))
+        return MultilinearExtension(self.num_vars - k, from_mont(out))
+
+    def add(self, other: "MultilinearExtension") -> "MultilinearExtension":  # :164-177
+        assert self.num_vars == other.num_vars, "Number of variables must match"
+        return MultilinearExtension(self.num_vars, [(a + b) % R_MOD for a, b in zip(self.evaluations, other.evaluations)])
+
+    def scalar_mul(self, s: int) -> "MultilinearExtension":  # :180-190
+        return MultilinearExtension(self.num_vars, [a * s % R_MOD for a in self.evaluations])
+
+    def sum_evaluations(self) -> int:  # :193-195
+        return sum(self.evaluations) % R_MOD
+
+
+# ----------------------------------------------------------------------------- sum-check
+@dataclass
+class SumCheckProof:
+    """src/sumcheck.rs:25-31"""
+    round_polynomials: List[List[int]]
+    final_evaluation: int
+
+
+class SumCheck:
+    """src/sumcheck.rs:15-110.  The closure is an MLE composition
+    sum_t coeff_t * prod_j tables[idx_tj] (each term of degree <= 3)."""
+
+    def __init__(self, num_vars: int, claimed_sum: int):
+        self.num_vars = num_vars
+        self.claimed_sum = claimed_sum % R_MOD
+
+    def prove(self, tables: Sequence[Sequence[int]], terms: Sequence[Tuple[int, Sequence[int]]],
+              transcript: Transcript, device: int = 0, return_challenges: bool = False):
+        nv = self.num_vars
+        arrs = [np.ascontiguousarray(t if isinstance(t, np.ndarray) else to_mont(list(t)), dtype=np.uint64)
+                for t in tables]
+        for a in arrs:
+            if len(a) != (1 << nv):
+                raise InvalidParameters("every table needs 2^num_vars entries")
+        ptrs = (N.U64P * max(1, len(arrs)))(*[N.p64(a) for a in arrs])
+        tt = (N.TnsTerm * max(1, len(terms)))()
+        for i, (coef, idx) in enumerate(terms):
+            tt[i].coeff = (C.c_uint64 * 4)(*[int(x) for x in to_mont([coef])[0]])
+            ix = list(idx) + [-1] * (3 - len(idx))
+            tt[i].tables = (C.c_int32 * 3)(*ix)
+        cl = to_mont([self.claimed_sum])[0]
+        rounds = np.zeros((max(1, nv), 4, 4), dtype=np.uint64)
+        fin = np.zeros(4, dtype=np.uint64)
+        ch = np.zeros((max(1, nv), 4), dtype=np.uint64)
+        _check(N.load().tns_sumcheck_prove(Context.get(device).handle, ptrs, len(arrs), nv, N.p64(cl), tt,
+                                           len(terms), transcript._h, N.p64(rounds), N.p64(fin), N.p64(ch)))
+        proof = SumCheckProof([from_mont(r) for r in rounds[:nv]], from_mont(fin)[0])
+        if return_challenges:
+            return proof, from_mont(ch[:nv]) if nv else []
+        return proof
+
+
+# ----------------------------------------------------------------------------- Twist
+@dataclass(frozen=True)
+class MemoryOp:
+    """src/twist.rs:17-20 (kind is "Read" or "Write")."""
+    kind: str
+    address: int
+    value: int
+
+
+class MemoryTrace:
+    """src/twist.rs:24-72"""
+
+    def __init__(self, memory_size: int):
+        if memory_size <= 0 or memory_size & (memory_size - 1):
+            raise AssertionError("Memory size must be power of 2")
+        self.memory_size = memory_size
+        self.operations: List[MemoryOp] = []
+        self._memory = [0] * memory_size
+
+    def write(self, address: int, value: int):
+        if address >= self.memory_size:
+            raise InvalidParameters("Address out of bounds")
+        self._memory[address] = value % R_MOD
+        self.operations.append(MemoryOp("Write", address, value % R_MOD))
+
+    def read(self, address: int) -> int:
+        if address >= self.memory_size:
+            raise InvalidParameters("Address out of bounds")
+        v = self._memory[address]
+        self.operations.append(MemoryOp("Read", address, v))
+        return v
+
+    def soa(self):
+        """(addr u64[n], value Montgomery (n,4), is_write u8[n]) -- the C-ABI layout."""
+        ops = self.operations
+        addr = np.array([o.address for o in ops], dtype=np.uint64)
+        val = to_mont([o.value for o in ops]) if ops else np.zeros((0, 4), dtype=np.uint64)
+        isw = np.array([1 if o.kind == "Write" else 0 for o in ops], dtype=np.uint8)
+        return addr, val, isw
+
+
+@dataclass
+class TwistProof:
+    """src/twist.rs:76-89 (+ diagnostics the reference computes but drops)."""
+    address_commitment: KZGCommitmentValue
+    value_commitment: KZGCommitmentValue
+    consistency_proof: SumCheckProof
+    opening_proofs: List[KZGProof]
+    final_evaluations: List[int]
+    opening_point: Optional[int] = None
+    sumcheck_challenges: List[int] = field(default_factory=list)
+    final_mle_evals: List[int] = field(default_factory=list)
+
+
+def _unpack_proof(pr: N.TnsProof, n_mles: int):
+    nr = pr.num_rounds
+    rounds = np.ctypeslib.as_array(pr.round_polynomials)[:nr]
+    comms = [np.ctypeslib.as_array(pr.commitments[i]).copy() for i in range(2)]
+    ops = [np.ctypeslib.as_array(pr.opening_proofs[i]).copy() for i in range(pr.num_openings)]
+    fe = [from_mont(np.ctypeslib.as_array(pr.final_evaluations[i]))[0] for i in range(pr.num_openings)]
+    return dict(
+        comms=[KZGCommitmentValue(_g1_from_proj(c), c) for c in comms],
+        sc=SumCheckProof([from_mont(r) for r in rounds], from_mont(np.ctypeslib.as_array(pr.final_evaluation))[0]),
+        openings=[KZGProof(_g1_from_proj(o)) for o in ops],
+        finals=fe,
+        z=from_mont(np.ctypeslib.as_array(pr.opening_point))[0] if pr.num_openings else None,
+        chals=from_mont(np.ctypeslib.as_array(pr.sumcheck_challenges)[:nr]) if nr else [],
+        mle=from_mont(np.ctypeslib.as_array(pr.final_mle_evals)[:n_mles]) if nr else [],
+    )
+
+
+class Twist:
+    """src/twist.rs:93-316 (prover)."""
+
+    def __init__(self, prover_params: ProverParams):
+        self.prover_params = prover_params
+
+    def prove_soa(self, addr: np.ndarray, value: np.ndarray, is_write: np.ndarray) -> TwistProof:
+        pp = self.prover_params
+        srs = pp.commitment_params.srs
+        addr = np.ascontiguousarray(addr, dtype=np.uint64)
+        value = np.ascontiguousarray(value, dtype=np.uint64).reshape(-1, 4)
+        is_write = np.ascontiguousarray(is_write, dtype=np.uint8)
+        n = len(addr)
+        pr = N.TnsProof()
+        _check(N.load().tns_twist_prove(
+            srs.ctx.handle, srs.handle, C.byref(pp.raw()),
+            N.p64(addr if n else np.zeros(1, dtype=np.uint64)), N.p64(_nonempty(value)),
+            N.p8(is_write if n else np.zeros(1, dtype=np.uint8)), n, C.byref(pr)))
+        u = _unpack_proof(pr, 3)
+        return TwistProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"], u["z"], u["chals"],
+                          u["mle"])
+
+    def prove(self, trace: MemoryTrace) -> TwistProof:
+        return self.prove_soa(*trace.soa())
+
+
+# ----------------------------------------------------------------------------- Shout
+@dataclass(frozen=True)
+class LookupOp:
+    """src/shout.rs:17-22"""
+    index: int
+    value: int
+
+
+class LookupTable:
+    """src/shout.rs:26-60"""
+
+    def __init__(self, entries: Sequence[int]):
+        self.entries = [int(e) % R_MOD for e in entries]
+        self.lookups: List[LookupOp] = []
+
+    def lookup(self, index: int) -> int:
+        if index >= len(self.entries):
+            raise InvalidParameters("Lookup index out of bounds")
+        v = self.entries[index]
+        self.lookups.append(LookupOp(index, v))
+        return v
+
+    def size(self) -> int:
+        return len(self.entries)
+
+
+@dataclass
+class ShoutProof:
+    """src/shout.rs:64-79"""
+    table_commitment: KZGCommitmentValue
+    index_commitment: KZGCommitmentValue
+    lookup_proof: SumCheckProof
+    opening_proofs: List[KZGProof]
+    final_evaluations: List[int]
+    opening_point: Optional[int] = None
+    sumcheck_challenges: List[int] = field(default_factory=list)
+
+
+class Shout:
+    """src/shout.rs:83-286 (prover)."""
+
+    def __init__(self, prover_params: ProverParams):
+        self.prover_params = prover_params
+
+    def prove_arrays(self, entries_mont: np.ndarray, indices: np.ndarray) -> ShoutProof:
+        pp = self.prover_params
+        srs = pp.commitment_params.srs
+        e = np.ascontiguousarray(entries_mont, dtype=np.uint64).reshape(-1, 4)
+        ix = np.ascontiguousarray(indices, dtype=np.uint64)
+        pr = N.TnsProof()
+        _check(N.load().tns_shout_prove(srs.ctx.handle, srs.handle, C.byref(pp.raw()), N.p64(_nonempty(e)), len(e),
+                                        N.p64(ix if len(ix) else np.zeros(1, dtype=np.uint64)), len(ix),
+                                        C.byref(pr)))
+        u = _unpack_proof(pr, 1)
+        return ShoutProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"], u["z"], u["chals"])
+
+    def prove(self, table: LookupTable) -> ShoutProof:
+        e = to_mont(table.entries) if table.entries else np.zeros((0, 4), dtype=np.uint64)
+        ix = np.array([l.index for l in table.lookups], dtype=np.uint64)
+        return self.prove_arrays(e, ix)
+
+
+def bench_trace(memory_size: int, n_ops: int):
+    """Synthetic trace of src/benchmarks.rs:88-99 as SoA arrays (addr, value Montgomery, is_write)."""
+    addr = np.empty(n_ops, dtype=np.uint64)
+    val = np.empty(n_ops, dtype=np.uint64)
+    isw = np.empty(n_ops, dtype=np.uint8)
+    if n_ops:
+        _check(N.load().tns_bench_trace(memory_size, n_ops, N.p64(addr), N.p64(val), N.p8(isw)))
+    return addr, fr_from_u64_array(val), isw
+
+
+__all__ = [
+    "R_MOD", "P_MOD", "FieldElement", "TwistAndShoutError", "InvalidParameters", "ProofGeneration",
+    "ProofVerification", "CommitmentError", "PolynomialError", "SumCheckError", "DeviceError", "Context",
+    "CommitmentParams", "ProverParams", "VerifierParams", "setup_params", "Transcript", "KZGCommitment",
+    "KZGCommitmentValue", "KZGProof", "msm", "poly_utils", "MultilinearExtension", "SumCheck", "SumCheckProof",
+    "MemoryOp", "MemoryTrace", "Twist", "TwistProof", "LookupOp", "LookupTable", "Shout", "ShoutProof",
+    "bench_trace", "to_mont", "from_mont", "fr_from_u64_array", "device_count",
+]

@@ -49,6 +49,8 @@ def lib():
         L = C.CDLL(path)
         L.orc_setup_num_powers.restype = C.c_size_t
         L.orc_siphash.restype = C.c_uint64
+        L.orc_siphash.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint64, C.c_int, C.c_int]
+        L.orc_chacha20_block.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p]
         _LIB = L
     return _LIB
 
@@ -198,3 +200,11 @@ def shout_prove(params, entries, indices):
                                _p(e), C.c_size_t(len(entries)), _p(ix), C.c_size_t(len(indices)),
                                C.byref(pr))
     return st, _proof_dict(pr, ("table_commitment", "index_commitment"))
+
+
+def horner(coeff_limbs, z_limbs):
+    c = np.ascontiguousarray(coeff_limbs, dtype=np.uint64).reshape(-1, 4)
+    z = np.ascontiguousarray(z_limbs, dtype=np.uint64).reshape(4)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().orc_horner(_p(c), C.c_size_t(len(c)), _p(z), _p(out))
+    return out

@@ -734,3 +734,6 @@ int orc_shout_prove(const uint64_t *g1, size_t n_powers, size_t max_ops, const u
   free(Tb); free(I);
   return st;
 }
+
+/* Horner evaluation (src/utils.rs:217-221), exposed for size-independent checks. */
+void orc_horner(const uint64_t *c, size_t n, const uint64_t z[4], uint64_t out[4]) { horner(c, n, z, out); }

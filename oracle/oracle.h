@@ -64,6 +64,7 @@ int orc_commit(const uint64_t *g1_powers, size_t n_powers, const uint64_t *coeff
 int orc_open(const uint64_t *g1_powers, size_t n_powers, const uint64_t *coeffs, size_t n,
              const uint64_t z[4], uint64_t value[4], uint64_t proof_affine[8]);
 void orc_commitment_hash(const uint64_t affine[8], uint64_t out[4]);
+void orc_horner(const uint64_t *coeffs, size_t n, const uint64_t z[4], uint64_t out[4]);
 
 /* src/polynomials.rs:85-161 */
 void orc_mle_evaluate(const uint64_t *evals, unsigned nv, const uint64_t *point, uint64_t out[4]);

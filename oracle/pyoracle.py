@@ -690,3 +690,44 @@ def shout_prove(params, entries, lookup_indices):
                 sumcheck_challenges=chals,
                 opening_point=opening[0] if opening else None,
                 table_poly=t_poly, index_poly=i_poly)
+
+
+# ----------------------------------------------------------------------------
+# Size-independent checks (test helpers, not part of the reference algorithm)
+# ----------------------------------------------------------------------------
+def barycentric_eval(ys, z: int) -> int:
+    """Value at z of the interpolant of ys on nodes 0..n-1, in O(n) (no coefficients).
+
+    f(z) = M(z) * sum_i y_i w_i / (z - i),  w_i = (-1)^(n-1-i) / (i! (n-1-i)!),
+    M(z) = prod_i (z - i); if z is a node, f(z) = y_z.  Used to check commitments
+    (z = tau) and openings at sizes the O(n^3) restatement cannot reach.
+    """
+    n = len(ys)
+    z %= R_MOD
+    if z < n:
+        return ys[z] % R_MOD
+    fact = [1] * n
+    for i in range(1, n):
+        fact[i] = fact[i - 1] * i % R_MOD
+    inv_fact_last = fr_inv(fact[n - 1])
+    inv_fact = [1] * n
+    inv_fact[n - 1] = inv_fact_last
+    for i in range(n - 1, 0, -1):
+        inv_fact[i - 1] = inv_fact[i] * i % R_MOD
+    # batch inverse of (z - i)
+    d = [(z - i) % R_MOD for i in range(n)]
+    pre = [1] * (n + 1)
+    for i in range(n):
+        pre[i + 1] = pre[i] * d[i] % R_MOD
+    inv_all = fr_inv(pre[n])
+    M = pre[n]
+    acc = 0
+    for i in range(n - 1, -1, -1):
+        di_inv = inv_all * pre[i] % R_MOD
+        inv_all = inv_all * d[i] % R_MOD
+        if ys[i] % R_MOD:
+            w = inv_fact[i] * inv_fact[n - 1 - i] % R_MOD
+            if (n - 1 - i) & 1:
+                w = R_MOD - w
+            acc = (acc + ys[i] * w % R_MOD * di_inv) % R_MOD
+    return acc * M % R_MOD

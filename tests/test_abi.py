@@ -1,0 +1,124 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/tns.h declares,
+and its host-side logic (transcript, hashes, conversions, trace generator, setup tau/seed)
+matches the oracle.  No device compute is called here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+import twist_and_shout as ts
+from twist_and_shout import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "tns.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tns_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = N.load()
+    syms = declared_symbols()
+    assert len(syms) >= 30
+    for s in syms:
+        assert hasattr(lib, s), s
+    bound = {name for name, _, _ in N.SIGNATURES}
+    assert set(syms) == bound, set(syms) ^ bound
+
+
+def test_version_and_no_silent_fallback():
+    lib = N.load()
+    assert lib.tns_version() >= 100
+    if lib.tns_device_count() == 0:
+        # without a device the product path must refuse, not compute on the CPU
+        h = C.c_void_p()
+        st = lib.tns_ctx_create(0, C.byref(h))
+        assert st == 101, N.last_error()
+        with pytest.raises(ts.TwistAndShoutError):
+            ts.Context(0)
+
+
+def test_host_transcript_matches_oracle():
+    t = ts.Transcript(bytes([7] * 32))
+    o = po.Transcript(bytes([7] * 32))
+    for i, x in enumerate([0, 1, 123, po.R_MOD - 1, 2**200 + 5]):
+        t.append_field_element(b"lbl%d" % i, x)
+        o.append_field_element(b"lbl%d" % i, x)
+        assert t.challenge_field_element(b"c%d" % i) == o.challenge_field_element(b"c%d" % i)
+    t.append_field_elements(b"sumcheck_round_0", [1, 2, 3, 4])
+    o.append_field_elements(b"sumcheck_round_0", [1, 2, 3, 4])
+    assert t.challenge_field_elements(b"opening_challenges", 3) == o.challenge_field_elements(
+        b"opening_challenges", 3)
+
+
+def test_setup_tau_and_seed_on_host(golden):
+    lib = N.load()
+    for L, s in golden["setup_params"].items():
+        raw = N.TnsParams()
+        st = lib.tns_setup_params(None, int(L), C.byref(raw), None)  # no SRS -> no device needed
+        assert st == 0, N.last_error()
+        assert ts.from_mont(np.array(list(raw.tau), dtype=np.uint64))[0] == int(s["tau"], 16)
+        assert bytes(raw.fiat_shamir_seed).hex() == s["fiat_shamir_seed"]
+        assert raw.max_operations == s["max_operations"] and raw.num_powers == s["n_powers"]
+
+
+def test_commitment_hash_matches_oracle(golden):
+    for case in golden["twist"].values():
+        for key in ("address_commitment", "value_commitment"):
+            P = case["proof"][key]
+            Pa = None if P is None else (int(P[0], 16), int(P[1], 16))
+            assert ts.KZGCommitmentValue(Pa).hash() == po.commitment_hash(Pa)
+
+
+def test_conversions_roundtrip():
+    vals = [0, 1, 2, 42, 2**63 + 11, 2**64 - 1]
+    m = ts.fr_from_u64_array(np.array(vals, dtype=np.uint64))
+    assert ts.from_mont(m) == vals
+    big = [po.R_MOD - 1, 2**253 + 7, 12345678901234567890123]
+    assert ts.from_mont(ts.to_mont(big)) == big
+    assert ts.from_mont(ts.to_mont([5, 9], ts.P_MOD), ts.P_MOD) == [5, 9]
+    rng = np.random.default_rng(1)
+    x = rng.integers(0, 2**63, size=10000, dtype=np.uint64)
+    assert ts.from_mont(ts.fr_from_u64_array(x))[:50] == [int(v) for v in x[:50]]
+
+
+def test_bench_trace_matches_reference_generator():
+    for mem, n in ((8, 50), (256, 256), (4, 15)):
+        addr, val, isw = ts.bench_trace(mem, n)
+        ops = po.benchmark_trace(mem, n)
+        assert [int(a) for a in addr] == [a for (_, a, _) in ops]
+        assert [int(w) for w in isw] == [w for (w, _, _) in ops]
+        assert ts.from_mont(val) == [v for (_, _, v) in ops]
+
+
+def test_memory_trace_and_lookup_table_bookkeeping():
+    # tests/twist_tests.rs:7-61, tests/shout_tests.rs:7-68
+    tr = ts.MemoryTrace(8)
+    tr.write(0, 42)
+    tr.write(1, 73)
+    assert tr.read(0) == 42 and tr.read(1) == 73
+    assert len(tr.operations) == 4
+    with pytest.raises(ts.InvalidParameters):
+        tr.read(100)
+    with pytest.raises(AssertionError):
+        ts.MemoryTrace(6)
+    t = ts.LookupTable([i * i for i in range(8)])
+    assert t.lookup(3) == 9 and t.size() == 8
+    with pytest.raises(ts.InvalidParameters):
+        t.lookup(8)
+    # MultilinearExtension host-side constructors (tests/polynomial_tests.rs:7-72, 133-151)
+    m = ts.MultilinearExtension.from_sparse(3, [(0, 10), (2, 30), (5, 60)])
+    assert m.evaluations == [10, 0, 30, 0, 0, 60, 0, 0]
+    assert ts.MultilinearExtension.one_hot(3, 5).evaluations[5] == 1
+    a = ts.MultilinearExtension.from_evaluations([1, 2])
+    b = ts.MultilinearExtension.from_evaluations([3, 4])
+    assert a.add(b).evaluations == [4, 6] and a.scalar_mul(3).evaluations == [3, 6]
+    assert a.sum_evaluations() == 3
+    with pytest.raises(AssertionError):
+        ts.MultilinearExtension.from_evaluations([1] * 7)
