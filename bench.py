@@ -1,0 +1,213 @@
+#!/usr/bin/env python3
+"""bench.py -- Twist prover ops/s (C4) + KZG MSM G1-scalar-pairs/s at 2^20 (C2) on MI355X.
+
+A "step" is one Twist::prove (src/twist.rs:107-252) of the synthetic read/write trace of
+ProtocolBenchmarks (src/benchmarks.rs:88-99) with the trace already resident in HBM:
+C4 = setup_params(22), MemoryTrace::new(2^22), 2^24 operations.  `value` is the
+Twist prover throughput (operations / second, metric as src/benchmarks.rs:26-28), summed
+over ranks.  Multi-GPU runs (torchrun, one process per GPU) prove independent traces per
+rank -- weak scaling, no data-path collective; the timing uses a barrier on both sides
+and the max over ranks.
+
+Extra fields (rank 0, N = 1): C2 MSM pairs/s at 2^20 (setup_params(18), Fr::rand scalars
+from ChaCha20Rng([7;32])), C3 Shout lookups/s (2^20-entry table, 2^20 lookups), the per-
+stage device-time breakdown, the roofline of the dominant kernel (HIP events on the
+library's stream; algorithmic bytes from SURVEY.md 8(d)), and the CPU baseline (the C
+oracle restating the reference algorithms, on a bounded sample).
+"""
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "multilinear-map-cryptography_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Twist prover ops/sec + KZG MSM G1-scalar-pairs/sec at 2^20, 1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--log-ops", type=int, default=24, help="Twist trace length 2^k (C4: 24)")
+    ap.add_argument("--no-extras", action="store_true", help="skip C2/C3 extras and the CPU baseline")
+    ap.add_argument("--cpu-baseline-ops", type=int, default=256, help="oracle sample size (C1: 256)")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    pg = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        pg = dist
+    return world, rank, local, pg
+
+
+def barrier_sync(pg, local):
+    if pg is not None:
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.synchronize(local)
+        pg.barrier()
+
+
+def max_over_ranks(pg, local, x):
+    if pg is None:
+        return x
+    import torch
+
+    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def roofline_from_profile(ts, ctx):
+    stages = {}
+    for s in ts.PROFILE_STAGES:
+        ms, n, b = ts.profile_read(ctx, s)
+        if n:
+            stages[s] = {"ms": ms, "launches": n, "alg_bytes": b}
+    if not stages:
+        return None, stages
+    dom = max(stages, key=lambda k: stages[k]["ms"])
+    d = stages[dom]
+    avg_s = d["ms"] / d["launches"] / 1e3
+    per_launch = d["alg_bytes"] / d["launches"]
+    achieved = per_launch / avg_s / 1e9
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            with open(pmc) as f:
+                traffic = json.load(f).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
+            "alg_bytes_per_launch": per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
+            "note": "dominant stage by device time; integer-VALU-bound (256-bit Montgomery), so the HBM "
+                    "fraction is low by construction -- see DESIGN.md"}
+    return roof, stages
+
+
+def cpu_baseline(n_ops):
+    """The C oracle (reference algorithms: O(N^3) Lagrange, per-term commit, closure sum-check)."""
+    from oracle import coracle as co
+    from oracle import pyoracle as po
+
+    mem = max(1, n_ops // 4)
+    L = max(0, (mem - 1).bit_length())
+    cp = co.setup_params(L)
+    ops = po.benchmark_trace(1 << L, n_ops)
+    t0 = time.perf_counter()
+    st, _ = co.twist_prove(cp, ops)
+    dt = time.perf_counter() - t0
+    assert st == 0
+    return {"value": round(n_ops / dt, 3), "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": f"Twist::prove of the {n_ops}-op ProtocolBenchmarks trace (setup_params({L})) by the "
+                      f"single-threaded C oracle restating the reference algorithms; {dt:.2f} s",
+            "host_cpu": platform.processor() or platform.machine(), "host_nproc": os.cpu_count()}
+
+
+def main():
+    args = parse()
+    world, rank, local, pg = dist_setup(args)
+    import twist_and_shout as ts
+
+    ctx = ts.Context.get(local)
+    log_ops = args.log_ops
+    n_ops = 1 << log_ops
+    L = log_ops - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
+    pp, _ = ts.setup_params(L, device=local)
+    addr, val, isw = ts.bench_trace(1 << L, n_ops)
+    d_addr, d_val, d_isw = ts.DeviceBuffer(ctx, addr), ts.DeviceBuffer(ctx, val), ts.DeviceBuffer(ctx, isw)
+
+    for _ in range(args.warmup):
+        ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
+    barrier_sync(pg, local)
+    ts.profile_enable(ctx, True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
+    barrier_sync(pg, local)
+    dt = time.perf_counter() - t0
+    breakdown = ctx.timing()
+    roof, stages = roofline_from_profile(ts, ctx)
+    ts.profile_enable(ctx, False)
+    dt_max = max_over_ranks(pg, local, dt)
+    total_ops = world * n_ops * args.steps
+    value = total_ops / dt_max
+
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u256 (8x u32 Montgomery, BN254 Fr/Fq)",
+        "data": "synthetic (src/benchmarks.rs:88-99 trace)",
+        "config": {"workload": f"C4: Twist::prove, 2^{log_ops}-op trace, setup_params({L}), trace resident in HBM",
+                   "log_ops": log_ops, "ops_per_gpu": n_ops, "parallelism": f"independent traces x{world}"},
+        "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_extras:
+        # C2: MSM 2^20 pairs (setup_params(18)); scalars = Fr::rand from ChaCha20Rng([7;32])
+        pp18, _ = ts.setup_params(18, device=local)
+        n = 1 << 20
+        sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
+        ts.msm_resident(pp18.commitment_params, sc, n)
+        reps = 10
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            ts.msm_resident(pp18.commitment_params, sc, n)
+        t_msm = (time.perf_counter() - t1) / reps
+        out["msm_pairs_per_sec_2^20"] = round(n / t_msm, 1)
+        out["msm_ms_2^20"] = round(t_msm * 1e3, 3)
+        # C3: Shout, 2^20 squares table, 2^20 lookups i % 2^20 (src/benchmarks.rs:167-177)
+        T = 1 << 20
+        entries = ts.fr_from_u64_array(np.arange(T, dtype=np.uint64) ** 2)
+        idx = np.arange(T, dtype=np.uint64)
+        d_e, d_i = ts.DeviceBuffer(ctx, entries), ts.DeviceBuffer(ctx, idx)
+        ts.shout_prove_resident(pp18, d_e, T, d_i, T)
+        t2 = time.perf_counter()
+        ts.shout_prove_resident(pp18, d_e, T, d_i, T)
+        t_sh = time.perf_counter() - t2
+        out["shout_lookups_per_sec_2^20"] = round(T / t_sh, 1)
+        out["shout_ms_2^20"] = round(t_sh * 1e3, 3)
+        # PCIe-inclusive Twist (host buffers through the C ABI), for DESIGN.md
+        t3 = time.perf_counter()
+        ts.Twist(pp).prove_soa(addr, val, isw)
+        out["twist_ops_per_sec_pcie_inclusive"] = round(n_ops / (time.perf_counter() - t3), 2)
+    if roof is not None:
+        out["roofline"] = roof
+        out["stages_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in stages.items()}
+    if rank == 0 and world == 1 and not args.no_extras:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_ops)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -168,12 +168,40 @@ int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
                     const uint64_t *entries, size_t n_entries, const uint64_t *indices,
                     size_t n_lookups, tns_proof *out);
 
+/* ---------------------------------------------------------------- device-resident inputs */
+/* The same provers on inputs already resident in HBM (device pointers, e.g. from
+ * tns_buffer_upload): the steady-state serving path, no PCIe in the prove. */
+typedef struct tns_buffer tns_buffer;
+int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer **out);
+void *tns_buffer_device_ptr(const tns_buffer *buf);
+void tns_buffer_free(tns_buffer *buf);
+int tns_twist_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
+                           const uint64_t *d_addr, const uint64_t *d_value,
+                           const uint8_t *d_is_write, size_t n_ops, tns_proof *out);
+int tns_shout_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
+                           const uint64_t *d_entries, size_t n_entries, const uint64_t *d_indices,
+                           size_t n_lookups, tns_proof *out);
+/* KZGCommitment::commit / MSM on device-resident scalars. */
+int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, size_t n,
+                   uint64_t out_proj[12]);
+
+/* ---------------------------------------------------------------- kernel timing */
+/* HIP-event timing of the named stages on the context stream ("msm_accumulate",
+ * "msm_sort", "msm_digits", "msm_reduce", "ntt_stage", "ntt_lds", "ntt_pointwise",
+ * "interp_tile", "sumcheck_round", "open_scan").  Enabling resets the totals. */
+int tns_profile_enable(tns_ctx *ctx, int on);
+int tns_profile_read(tns_ctx *ctx, const char *stage, double *total_ms, uint64_t *launches,
+                     double *algorithmic_bytes);
+
 /* ---------------------------------------------------------------- host utilities (no device) */
 /* Batch conversions between integers and Montgomery-form Fr / Fq (multi-threaded). */
 void tns_fr_from_u64(const uint64_t *in, size_t n, uint64_t *out_mont);
 void tns_fr_from_canonical(const uint64_t *in, size_t n, uint64_t *out_mont);
 void tns_fr_to_canonical(const uint64_t *in_mont, size_t n, uint64_t *out);
 void tns_fq_to_canonical(const uint64_t *in_mont, size_t n, uint64_t *out);
+/* n successive `Fr::rand` draws (ark-ff 0.4.2 UniformRand) from ChaCha20Rng::from_seed(seed)
+ * -- the synthetic scalars of the C2 MSM configuration (seed [7;32]). */
+void tns_fr_rand_batch(const uint8_t seed[32], size_t n, uint64_t *out_mont);
 /* The synthetic read/write trace of ProtocolBenchmarks (src/benchmarks.rs:88-99):
  * op i writes Fr(42 i) to i % memory_size when i % 3 == 0, else reads (i / 2) % memory_size
  * and records the current memory value.  value_u64 holds the values as integers. */

@@ -25,6 +25,11 @@ struct tns_srs {
 struct tns_transcript {
   tns::HostTranscript t;
 };
+struct tns_buffer {
+  tns::DevBuf buf;
+  size_t bytes = 0;
+  int device = 0;
+};
 
 namespace tns {
 
@@ -425,124 +430,234 @@ __global__ void k_write_flags(const uint8_t *__restrict__ in, Fr *__restrict__ o
     out[i] = (i < n_in && in[i]) ? Fr::one() : Fr::zero();
 }
 
+__global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, uint64_t bound,
+                                  unsigned *__restrict__ bad) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    if (idx[i] >= bound) *bad = 1;
+}
+
+// Twist::prove (src/twist.rs:107-252).  kind: where addr/value/is_write live (H2D or D2D).
+static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *addr,
+                       const uint64_t *value, const uint8_t *is_write, size_t n_ops, tns_proof *out,
+                       hipMemcpyKind kind) {
+  Timer total;
+  CtxScope g(&ctx->c);
+  Ctx *c = &ctx->c;
+  hipStream_t st = c->stream;
+  std::memset(out, 0, sizeof *out);
+  if (n_ops > params->max_operations)  // src/twist.rs:108-112
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many operations");
+  const size_t N = next_pow2(n_ops);  // :141 next_power_of_two().max(1)
+  const unsigned nv = ilog2_exact(N);
+  if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "trace too long");
+  double *tm = ctx->timing;
+  for (int i = 0; i < 6; i++) tm[i] = 0;
+  // ---- SoA extraction / padding into the resident workspace (src/twist.rs:115-148)
+  Timer t_h2d;
+  DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
+         &d_v = c->prove_ws[3], &d_o = c->prove_ws[4], &d_ca = c->prove_ws[5], &d_cv = c->prove_ws[6],
+         &d_s = c->prove_ws[7];
+  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * N), *V = (Fr *)d_v.ensure(sizeof(Fr) * N), *O = (Fr *)d_o.ensure(sizeof(Fr) * N);
+  const uint64_t *ar = addr;
+  const uint8_t *fl = is_write;
+  if (kind == hipMemcpyHostToDevice) {
+    uint64_t *dar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
+    uint8_t *dfl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
+    if (n_ops) {
+      TNS_HIP(hipMemcpyAsync(dar, addr, 8 * n_ops, hipMemcpyHostToDevice, st));
+      TNS_HIP(hipMemcpyAsync(dfl, is_write, n_ops, hipMemcpyHostToDevice, st));
+    }
+    ar = dar;
+    fl = dfl;
+  }
+  if (n_ops) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
+  fr_fill_zero_dev(c, A, N);
+  to_mont_u64_dev(c, ar, A, n_ops);
+  if (N > n_ops) fr_fill_zero_dev(c, V + n_ops, N - n_ops);
+  k_write_flags<<<grid_for(N, 256), 256, 0, st>>>(fl, O, n_ops, N);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[0] = t_h2d.ms();
+  // ---- vector_to_polynomial x2 (src/twist.rs:151-152)
+  Timer t_int;
+  Fr *CA = (Fr *)d_ca.ensure(sizeof(Fr) * N), *CV = (Fr *)d_cv.ensure(sizeof(Fr) * N);
+  interpolate_consecutive_dev(c, A, N, CA);
+  interpolate_consecutive_dev(c, V, N, CV);
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[1] = t_int.ms();
+  // ---- commit x2 (src/twist.rs:155-163)
+  Timer t_com;
+  G1Affine Ca = commit_dev(c, srs->s, CA, N);
+  G1Affine Cv = commit_dev(c, srs->s, CV, N);
+  store_proj(Ca, out->commitments[0]);
+  store_proj(Cv, out->commitments[1]);
+  tm[2] = t_com.ms();
+  // ---- transcript (src/twist.rs:170-174)
+  HostTranscript tr;
+  tr.append_label("address_commitment");
+  tr.append_fr(commitment_hash(Ca));
+  tr.append_label("value_commitment");
+  tr.append_fr(commitment_hash(Cv));
+  // ---- sum-check over the addr / value / op-type MLEs + openings (src/twist.rs:177-243)
+  Fr *mles[3] = {A, V, O};
+  fill_common_tail(c, srs->s, tr, mles, 3, nv, CA, N, CV, N, out, tm, d_s);
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[5] = total.ms();
+}
+
 int tns_twist_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *addr,
                     const uint64_t *value, const uint8_t *is_write, size_t n_ops, tns_proof *out) {
   return guarded([&]() {
-    Timer total;
-    CtxScope g(&ctx->c);
-    Ctx *c = &ctx->c;
-    hipStream_t st = c->stream;
-    std::memset(out, 0, sizeof *out);
-    if (n_ops > params->max_operations)  // src/twist.rs:108-112
-      throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many operations");
-    const size_t N = next_pow2(n_ops);  // :141 next_power_of_two().max(1)
-    const unsigned nv = ilog2_exact(N);
-    if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "trace too long");
-    double *tm = ctx->timing;
-    for (int i = 0; i < 6; i++) tm[i] = 0;
-    // ---- H2D + SoA extraction/padding (src/twist.rs:115-148)
-    Timer t_h2d;
-    DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
-           &d_v = c->prove_ws[3], &d_o = c->prove_ws[4], &d_ca = c->prove_ws[5], &d_cv = c->prove_ws[6],
-           &d_s = c->prove_ws[7];
-    uint64_t *ar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
-    uint8_t *fl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
-    Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * N), *V = (Fr *)d_v.ensure(sizeof(Fr) * N), *O = (Fr *)d_o.ensure(sizeof(Fr) * N);
-    if (n_ops) {
-      TNS_HIP(hipMemcpyAsync(ar, addr, 8 * n_ops, hipMemcpyHostToDevice, st));
-      TNS_HIP(hipMemcpyAsync(fl, is_write, n_ops, hipMemcpyHostToDevice, st));
-      TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, hipMemcpyHostToDevice, st));
-    }
-    fr_fill_zero_dev(c, A, N);
-    to_mont_u64_dev(c, ar, A, n_ops);
-    if (N > n_ops) fr_fill_zero_dev(c, V + n_ops, N - n_ops);
-    k_write_flags<<<grid_for(N, 256), 256, 0, st>>>(fl, O, n_ops, N);
-    TNS_LAUNCH_CHECK();
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[0] = t_h2d.ms();
-    // ---- vector_to_polynomial x2 (src/twist.rs:151-152)
-    Timer t_int;
-    Fr *CA = (Fr *)d_ca.ensure(sizeof(Fr) * N), *CV = (Fr *)d_cv.ensure(sizeof(Fr) * N);
-    interpolate_consecutive_dev(c, A, N, CA);
-    interpolate_consecutive_dev(c, V, N, CV);
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[1] = t_int.ms();
-    // ---- commit x2 (src/twist.rs:155-163)
-    Timer t_com;
-    G1Affine Ca = commit_dev(c, srs->s, CA, N);
-    G1Affine Cv = commit_dev(c, srs->s, CV, N);
-    store_proj(Ca, out->commitments[0]);
-    store_proj(Cv, out->commitments[1]);
-    tm[2] = t_com.ms();
-    // ---- transcript (src/twist.rs:170-174)
-    HostTranscript tr;
-    tr.append_label("address_commitment");
-    tr.append_fr(commitment_hash(Ca));
-    tr.append_label("value_commitment");
-    tr.append_fr(commitment_hash(Cv));
-    // ---- sum-check over the addr / value / op-type MLEs + openings (src/twist.rs:177-243)
-    Fr *mles[3] = {A, V, O};
-    fill_common_tail(c, srs->s, tr, mles, 3, nv, CA, N, CV, N, out, tm, d_s);
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[5] = total.ms();
+    twist_core(ctx, srs, params, addr, value, is_write, n_ops, out, hipMemcpyHostToDevice);
     return TNS_OK;
   });
+}
+
+int tns_twist_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *d_addr,
+                           const uint64_t *d_value, const uint8_t *d_is_write, size_t n_ops, tns_proof *out) {
+  return guarded([&]() {
+    twist_core(ctx, srs, params, d_addr, d_value, d_is_write, n_ops, out, hipMemcpyDeviceToDevice);
+    return TNS_OK;
+  });
+}
+
+// Shout::prove (src/shout.rs:97-222)
+static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *entries,
+                       size_t n_entries, const uint64_t *indices, size_t n_lookups, tns_proof *out,
+                       hipMemcpyKind kind) {
+  Timer total;
+  CtxScope g(&ctx->c);
+  Ctx *c = &ctx->c;
+  hipStream_t st = c->stream;
+  std::memset(out, 0, sizeof *out);
+  if (n_lookups > params->max_operations)  // src/shout.rs:98-102
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many lookup operations");
+  const size_t T = next_pow2(n_entries), M = next_pow2(n_lookups);  // :105, :116
+  const unsigned nv = ilog2_exact(M);
+  if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many lookups");
+  double *tm = ctx->timing;
+  for (int i = 0; i < 6; i++) tm[i] = 0;
+  Timer t_h2d;
+  DevBuf &d_idx_raw = c->prove_ws[0], &d_bad = c->prove_ws[1], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3],
+         &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
+  Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * T), *I = (Fr *)d_i.ensure(sizeof(Fr) * M);
+  fr_fill_zero_dev(c, TB, T);
+  fr_fill_zero_dev(c, I, M);
+  if (n_entries) TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
+  if (n_lookups) {
+    const uint64_t *ir = indices;
+    if (kind == hipMemcpyHostToDevice) {
+      uint64_t *dir = (uint64_t *)d_idx_raw.ensure(8 * n_lookups);
+      TNS_HIP(hipMemcpyAsync(dir, indices, 8 * n_lookups, hipMemcpyHostToDevice, st));
+      ir = dir;
+    }
+    // LookupTable::lookup bounds (src/shout.rs:44-50)
+    unsigned *bad = (unsigned *)d_bad.ensure(sizeof(unsigned));
+    TNS_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
+    k_max_index_check<<<grid_for(n_lookups, 256), 256, 0, st>>>(ir, n_lookups, n_entries, bad);
+    TNS_LAUNCH_CHECK();
+    unsigned hbad = 0;
+    TNS_HIP(hipMemcpyAsync(&hbad, bad, sizeof hbad, hipMemcpyDeviceToHost, st));
+    TNS_HIP(hipStreamSynchronize(st));
+    if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
+    to_mont_u64_dev(c, ir, I, n_lookups);
+  }
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[0] = t_h2d.ms();
+  Timer t_int;
+  Fr *CT = (Fr *)d_ct.ensure(sizeof(Fr) * T), *CI = (Fr *)d_ci.ensure(sizeof(Fr) * M);
+  interpolate_consecutive_dev(c, TB, T, CT);
+  interpolate_consecutive_dev(c, I, M, CI);
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[1] = t_int.ms();
+  Timer t_com;
+  G1Affine Ct = commit_dev(c, srs->s, CT, T);  // table first (src/shout.rs:125-133)
+  G1Affine Ci = commit_dev(c, srs->s, CI, M);
+  store_proj(Ct, out->commitments[0]);
+  store_proj(Ci, out->commitments[1]);
+  tm[2] = t_com.ms();
+  HostTranscript tr;
+  tr.append_label("table_commitment");
+  tr.append_fr(commitment_hash(Ct));
+  tr.append_label("index_commitment");
+  tr.append_fr(commitment_hash(Ci));
+  Fr *mles[1] = {I};  // the closure evaluates only the index MLE (src/shout.rs:175)
+  fill_common_tail(c, srs->s, tr, mles, 1, nv, CT, T, CI, M, out, tm, d_s);
+  TNS_HIP(hipStreamSynchronize(st));
+  tm[5] = total.ms();
 }
 
 int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *entries,
                     size_t n_entries, const uint64_t *indices, size_t n_lookups, tns_proof *out) {
   return guarded([&]() {
-    Timer total;
-    CtxScope g(&ctx->c);
-    Ctx *c = &ctx->c;
-    hipStream_t st = c->stream;
-    std::memset(out, 0, sizeof *out);
-    if (n_lookups > params->max_operations)  // src/shout.rs:98-102
-      throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many lookup operations");
-    for (size_t i = 0; i < n_lookups; i++)  // LookupTable::lookup bounds (src/shout.rs:44-50)
-      if (indices[i] >= n_entries) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
-    const size_t T = next_pow2(n_entries), M = next_pow2(n_lookups);  // :105, :116
-    const unsigned nv = ilog2_exact(M);
-    if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many lookups");
-    double *tm = ctx->timing;
-    for (int i = 0; i < 6; i++) tm[i] = 0;
-    Timer t_h2d;
-    DevBuf &d_idx_raw = c->prove_ws[0], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3], &d_ct = c->prove_ws[5],
-           &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
-    uint64_t *ir = (uint64_t *)d_idx_raw.ensure(8 * (n_lookups ? n_lookups : 1));
-    Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * T), *I = (Fr *)d_i.ensure(sizeof(Fr) * M);
-    fr_fill_zero_dev(c, TB, T);
-    fr_fill_zero_dev(c, I, M);
-    if (n_entries) TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, hipMemcpyHostToDevice, st));
-    if (n_lookups) {
-      TNS_HIP(hipMemcpyAsync(ir, indices, 8 * n_lookups, hipMemcpyHostToDevice, st));
-      to_mont_u64_dev(c, ir, I, n_lookups);
-    }
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[0] = t_h2d.ms();
-    Timer t_int;
-    Fr *CT = (Fr *)d_ct.ensure(sizeof(Fr) * T), *CI = (Fr *)d_ci.ensure(sizeof(Fr) * M);
-    interpolate_consecutive_dev(c, TB, T, CT);
-    interpolate_consecutive_dev(c, I, M, CI);
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[1] = t_int.ms();
-    Timer t_com;
-    G1Affine Ct = commit_dev(c, srs->s, CT, T);  // table first (src/shout.rs:125-133)
-    G1Affine Ci = commit_dev(c, srs->s, CI, M);
-    store_proj(Ct, out->commitments[0]);
-    store_proj(Ci, out->commitments[1]);
-    tm[2] = t_com.ms();
-    HostTranscript tr;
-    tr.append_label("table_commitment");
-    tr.append_fr(commitment_hash(Ct));
-    tr.append_label("index_commitment");
-    tr.append_fr(commitment_hash(Ci));
-    Fr *mles[1] = {I};  // the closure evaluates only the index MLE (src/shout.rs:175)
-    fill_common_tail(c, srs->s, tr, mles, 1, nv, CT, T, CI, M, out, tm, d_s);
-    TNS_HIP(hipStreamSynchronize(st));
-    tm[5] = total.ms();
+    shout_core(ctx, srs, params, entries, n_entries, indices, n_lookups, out, hipMemcpyHostToDevice);
     return TNS_OK;
   });
+}
+
+int tns_shout_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *d_entries,
+                           size_t n_entries, const uint64_t *d_indices, size_t n_lookups, tns_proof *out) {
+  return guarded([&]() {
+    shout_core(ctx, srs, params, d_entries, n_entries, d_indices, n_lookups, out, hipMemcpyDeviceToDevice);
+    return TNS_OK;
+  });
+}
+
+// ---------------------------------------------------------------- device buffers
+int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer **out) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    tns_buffer *b = new tns_buffer();
+    b->device = ctx->c.device;
+    b->bytes = bytes;
+    try {
+      b->buf.ensure(bytes ? bytes : 16);
+      if (bytes) TNS_HIP(hipMemcpy(b->buf.p, host, bytes, hipMemcpyHostToDevice));
+    } catch (...) {
+      delete b;
+      throw;
+    }
+    *out = b;
+    return TNS_OK;
+  });
+}
+void *tns_buffer_device_ptr(const tns_buffer *b) { return b ? b->buf.p : nullptr; }
+void tns_buffer_free(tns_buffer *b) {
+  if (!b) return;
+  (void)hipSetDevice(b->device);
+  delete b;
+}
+
+int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, size_t n, uint64_t out[12]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    store_proj(commit_dev(&ctx->c, srs->s, (const Fr *)d_scalars, n), out);
+    return TNS_OK;
+  });
+}
+
+// ---------------------------------------------------------------- kernel timing (HIP events)
+int tns_profile_enable(tns_ctx *ctx, int on) {
+  ctx->c.prof.enabled = on != 0;
+  ctx->c.prof.reset();
+  return TNS_OK;
+}
+int tns_profile_read(tns_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches, double *alg_bytes) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.prof.collect();
+    auto it = ctx->c.prof.totals.find(kernel);
+    bool f = it != ctx->c.prof.totals.end();
+    *total_ms = f ? it->second.ms : 0.0;
+    *launches = f ? it->second.launches : 0;
+    *alg_bytes = f ? it->second.bytes : 0.0;
+    return TNS_OK;
+  });
+}
+
+// n draws of ark-ff UniformRand for Fr from one ChaCha20Rng::from_seed(seed) stream (host)
+void tns_fr_rand_batch(const uint8_t seed[32], size_t n, uint64_t *out_mont) {
+  host_fr_rand_stream(seed, n, (Fr *)out_mont);
 }
 
 // ---------------------------------------------------------------- host utilities

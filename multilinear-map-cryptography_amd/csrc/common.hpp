@@ -6,6 +6,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -83,6 +84,62 @@ struct Srs {
   int device = 0;
 };
 
+// Per-kernel device time from HIP events recorded on the context stream around
+// the launches of one named stage (enabled by tns_profile_enable; used by bench.py
+// for the roofline's live kernel duration).
+struct KernelProfiler {
+  bool enabled = false;
+  struct Rec {
+    std::string name;
+    hipEvent_t a, b;
+    double bytes;
+  };
+  struct Tot {
+    double ms = 0, bytes = 0;
+    uint64_t launches = 0;
+  };
+  std::vector<Rec> pending;
+  std::map<std::string, Tot> totals;  // name -> (device ms, launches, algorithmic bytes)
+  void reset() {
+    collect();
+    totals.clear();
+  }
+  void collect() {
+    for (auto &r : pending) {
+      float ms = 0.f;
+      if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+        auto &t = totals[r.name];
+        t.ms += ms;
+        t.launches += 1;
+        t.bytes += r.bytes;
+      }
+      (void)hipEventDestroy(r.a);
+      (void)hipEventDestroy(r.b);
+    }
+    pending.clear();
+  }
+};
+
+struct ProfScope {
+  KernelProfiler *p = nullptr;
+  hipStream_t s;
+  KernelProfiler::Rec r;
+  ProfScope(KernelProfiler &prof, hipStream_t st, const char *name, double alg_bytes) : s(st) {
+    if (!prof.enabled) return;
+    p = &prof;
+    r.name = name;
+    r.bytes = alg_bytes;
+    (void)hipEventCreate(&r.a);
+    (void)hipEventCreate(&r.b);
+    (void)hipEventRecord(r.a, s);
+  }
+  ~ProfScope() {
+    if (!p) return;
+    (void)hipEventRecord(r.b, s);
+    p->pending.push_back(r);
+  }
+};
+
 struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -94,8 +151,14 @@ struct Ctx {
   DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
+  KernelProfiler prof;
   ~Ctx();
 };
+#define TNS_CAT2(a, b) a##b
+#define TNS_CAT(a, b) TNS_CAT2(a, b)
+// TNS_PROF(ctx, "stage", algorithmic_bytes_of_this_launch)
+#define TNS_PROF(ctx, name, bytes) \
+  ::tns::ProfScope TNS_CAT(_tns_prof_, __LINE__)((ctx)->prof, (ctx)->stream, name, (double)(bytes))
 
 // RAII device guard + lock
 struct CtxScope {
@@ -164,6 +227,7 @@ struct HostTranscript {
 Fr commitment_hash(const G1Affine &a);
 Fr host_fr_rand_chacha(const uint8_t seed[32], uint8_t *fs_seed_out /* nullable: next 32 bytes */);
 uint64_t siphash13_keys00(const uint8_t *msg, size_t n);
+void host_fr_rand_stream(const uint8_t seed[32], size_t n, Fr *out);
 void chacha20_block_host(const uint32_t key[8], uint64_t counter, uint32_t out[16]);
 // Lagrange interpolation of 4 points (0..3) for sum-check round polys (host, exact).
 void interpolate4_host(const Fr e[4], Fr out[4]);

@@ -160,15 +160,21 @@ static void ntt_blocks(Ctx *c, Fr *x, unsigned s, size_t nb, bool inverse) {
   const size_t nbf = total >> 1;
   if (!inverse) {
     for (int lh = (int)s - 1; lh > lds_hi; lh--) {
+      TNS_PROF(c, "ntt_stage", 64.0 * total);
       k_ntt_stage<false><<<grid_for(nbf, 256), 256, 0, c->stream>>>(x, nbf, (unsigned)lh, tw, lmax);
       TNS_LAUNCH_CHECK();
     }
+    TNS_PROF(c, "ntt_lds", 64.0 * total);
     k_ntt_lds<false><<<(unsigned)ntiles, 256, 0, c->stream>>>(x, (unsigned)tile_len, lds_hi, tw, lmax);
     TNS_LAUNCH_CHECK();
   } else {
+    {
+    TNS_PROF(c, "ntt_lds", 64.0 * total);
     k_ntt_lds<true><<<(unsigned)ntiles, 256, 0, c->stream>>>(x, (unsigned)tile_len, lds_hi, tw, lmax);
     TNS_LAUNCH_CHECK();
+    }
     for (int lh = lds_hi + 1; lh < (int)s; lh++) {
+      TNS_PROF(c, "ntt_stage", 64.0 * total);
       k_ntt_stage<true><<<grid_for(nbf, 256), 256, 0, c->stream>>>(x, nbf, (unsigned)lh, tw, lmax);
       TNS_LAUNCH_CHECK();
     }
@@ -185,6 +191,7 @@ __global__ void __launch_bounds__(256) k_pointwise(Fr *__restrict__ x, const Fr 
 }
 static void pointwise_blocks(Ctx *c, Fr *x, const Fr *w, unsigned s, size_t nb) {
   size_t total = nb << s;
+  TNS_PROF(c, "ntt_pointwise", 96.0 * total);
   k_pointwise<<<grid_for(total, 256), 256, 0, c->stream>>>(x, w, s, total);
   TNS_LAUNCH_CHECK();
 }
@@ -517,8 +524,11 @@ void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs) {
   const Fr *tw = c->twiddles.as<Fr>();
   const unsigned tile_log = log_n < INT_TILE_LOG ? log_n : INT_TILE_LOG;
   const unsigned tile = 1u << tile_log;
-  k_interp_tile<<<(unsigned)(n / tile), 256, 0, st>>>(A, tile, tile_log, fact, ifact, lv, tw, lmax);
-  TNS_LAUNCH_CHECK();
+  {
+    TNS_PROF(c, "interp_tile", 64.0 * n);
+    k_interp_tile<<<(unsigned)(n / tile), 256, 0, st>>>(A, tile, tile_log, fact, ifact, lv, tw, lmax);
+    TNS_LAUNCH_CHECK();
+  }
   Fr *X = X2, *Y = X2 + n;
   for (unsigned l = tile_log; l < log_n; l++) {
     const size_t m = (size_t)1 << l;

@@ -245,6 +245,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
       tt.out[i] = dst[i];
     }
     const unsigned g = grid_for(P, 256, 2048);
+    TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
     if (rnd == 0) {
       if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
     } else {

@@ -164,15 +164,15 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
 
 // per (window, group): sum_{j in group} (j+1) B_j
 __global__ void __launch_bounds__(256) k_bucket_reduce(const G1Xyzz *__restrict__ buckets, int W,
-                                                       int half_buckets, G1Xyzz *__restrict__ out) {
-  const int groups = half_buckets / RED_L;
+                                                       int half_buckets, int red_l, G1Xyzz *__restrict__ out) {
+  const int groups = half_buckets / red_l;
   for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)W * groups;
        id += (size_t)gridDim.x * blockDim.x) {
     int w = (int)(id / groups), g = (int)(id % groups);
     const G1Xyzz *B = buckets + (size_t)w * half_buckets;
-    int a = g * RED_L;
+    int a = g * red_l;
     G1Xyzz run = G1Xyzz::inf(), acc = G1Xyzz::inf();
-    for (int j = a + RED_L - 1; j >= a; j--) {
+    for (int j = a + red_l - 1; j >= a; j--) {
       run = xyzz_add(run, B[j]);
       acc = xyzz_add(acc, run);
     }
@@ -247,36 +247,46 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
   G1Xyzz *buckets = (G1Xyzz *)ctx->msm_ws[5].ensure(sizeof(G1Xyzz) * P.nb);
   const size_t nchunks = (total + ACC_K - 1) / ACC_K;
   HeadTail *ht = (HeadTail *)ctx->msm_ws[6].ensure(sizeof(HeadTail) * nchunks);
-  const int groups = half / RED_L > 0 ? half / RED_L : 1;
+  const int red_l = half < RED_L ? half : RED_L;
+  const int groups = half / red_l;
   G1Xyzz *parts = (G1Xyzz *)ctx->msm_ws[7].ensure(sizeof(G1Xyzz) * (size_t)P.W * groups);
   G1Xyzz *wsum = (G1Xyzz *)ctx->msm_ws[8].ensure(sizeof(G1Xyzz) * P.W);
 
-  k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, keys, vals);
-  TNS_LAUNCH_CHECK();
+  {
+    TNS_PROF(ctx, "msm_digits", 32.0 * n + 8.0 * total);
+    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, keys, vals);
+    TNS_LAUNCH_CHECK();
+  }
 
   size_t temp_bytes = 0;
   TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total,
                                              0, P.end_bit, st));
   void *temp = ctx->msm_ws[9].ensure(temp_bytes);
-  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
-                                             P.end_bit, st));
+  {
+    TNS_PROF(ctx, "msm_sort", 16.0 * total);
+    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
+                                               P.end_bit, st));
+  }
 
   TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
   k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
   TNS_LAUNCH_CHECK();
-  k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
-                                                                 points, buckets, ht, nchunks);
-  TNS_LAUNCH_CHECK();
+  {
+    TNS_PROF(ctx, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
+    k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
+                                                                   points, buckets, ht, nchunks);
+    TNS_LAUNCH_CHECK();
+  }
   k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, buckets, P.nb);
   TNS_LAUNCH_CHECK();
-  if (half >= RED_L) {
-    k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, parts);
+  {
+    TNS_PROF(ctx, "msm_reduce", 128.0 * P.nb);
+    k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, red_l,
+                                                                                  parts);
     TNS_LAUNCH_CHECK();
     k_window_sum<<<P.W, 256, 0, st>>>(parts, groups, wsum);
-  } else {
-    throw Error(TNS_ERR_COMMITMENT, "MSM window too small");
+    TNS_LAUNCH_CHECK();
   }
-  TNS_LAUNCH_CHECK();
   std::vector<G1Xyzz> S(P.W);
   TNS_HIP(hipMemcpyAsync(S.data(), wsum, sizeof(G1Xyzz) * P.W, hipMemcpyDeviceToHost, st));
   TNS_HIP(hipStreamSynchronize(st));

@@ -68,6 +68,7 @@ static void suffix_scan(Ctx *ctx, const Fr *c, size_t n, const Fr &z, Fr *out, i
   // two arrays of C per level in one allocation
   Fr *L = (Fr *)ctx->scratch[depth].ensure(sizeof(Fr) * 2 * C);
   Fr *S = L + C;
+  TNS_PROF(ctx, "open_scan", 96.0 * n);
   k_scan_chunk_local<<<grid_for(C, 256, 1u << 30), 256, 0, ctx->stream>>>(c, n, z, L, C);
   TNS_LAUNCH_CHECK();
   Fr Z = pow_u64(z, SCAN_K);

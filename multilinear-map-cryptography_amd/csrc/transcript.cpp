@@ -99,6 +99,11 @@ Fr host_fr_rand_chacha(const uint8_t seed[32], uint8_t *fs_seed_out) {
   return r;
 }
 
+void host_fr_rand_stream(const uint8_t seed[32], size_t n, Fr *out) {
+  ChaChaStream g(seed);
+  for (size_t i = 0; i < n; i++) out[i] = fr_rand(g);
+}
+
 uint64_t siphash13_keys00(const uint8_t *m, size_t n) {
   uint64_t v0 = 0x736f6d6570736575ULL, v1 = 0x646f72616e646f6dULL;
   uint64_t v2 = 0x6c7967656e657261ULL, v3 = 0x7465646279746573ULL;

@@ -654,6 +654,75 @@ class Shout:
         return self.prove_arrays(e, ix)
 
 
+class DeviceBuffer:
+    """An input array resident in HBM (tns_buffer_upload)."""
+
+    def __init__(self, ctx: Context, host: np.ndarray):
+        host = np.ascontiguousarray(host)
+        self.ctx = ctx
+        self.nbytes = host.nbytes
+        self.handle = C.c_void_p()
+        _check(N.load().tns_buffer_upload(ctx.handle, host.ctypes.data_as(C.c_void_p), host.nbytes,
+                                          C.byref(self.handle)))
+        self.ptr = N.load().tns_buffer_device_ptr(self.handle)
+
+    def __del__(self):
+        try:
+            N.load().tns_buffer_free(self.handle)
+        except Exception:
+            pass
+
+
+def twist_prove_resident(pp: ProverParams, addr: DeviceBuffer, value: DeviceBuffer, is_write: DeviceBuffer,
+                         n_ops: int) -> N.TnsProof:
+    """Twist::prove on a trace already resident in HBM; returns the raw C proof struct."""
+    srs = pp.commitment_params.srs
+    pr = N.TnsProof()
+    _check(N.load().tns_twist_prove_device(srs.ctx.handle, srs.handle, C.byref(pp.raw()), addr.ptr, value.ptr,
+                                           is_write.ptr, n_ops, C.byref(pr)))
+    return pr
+
+
+def shout_prove_resident(pp: ProverParams, entries: DeviceBuffer, n_entries: int, indices: DeviceBuffer,
+                         n_lookups: int) -> N.TnsProof:
+    srs = pp.commitment_params.srs
+    pr = N.TnsProof()
+    _check(N.load().tns_shout_prove_device(srs.ctx.handle, srs.handle, C.byref(pp.raw()), entries.ptr, n_entries,
+                                           indices.ptr, n_lookups, C.byref(pr)))
+    return pr
+
+
+def msm_resident(params: CommitmentParams, scalars: DeviceBuffer, n: int) -> np.ndarray:
+    out = np.zeros(12, dtype=np.uint64)
+    _check(N.load().tns_msm_device(params.srs.ctx.handle, params.srs.handle, scalars.ptr, n, N.p64(out)))
+    return out
+
+
+def profile_enable(ctx: Context, on: bool = True):
+    N.load().tns_profile_enable(ctx.handle, 1 if on else 0)
+
+
+PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_reduce", "ntt_stage", "ntt_lds",
+                  "ntt_pointwise", "interp_tile", "sumcheck_round", "open_scan"]
+
+
+def profile_read(ctx: Context, stage: str):
+    """(device ms, launches, algorithmic bytes) accumulated for one stage since profile_enable."""
+    ms = C.c_double()
+    n = C.c_uint64()
+    b = C.c_double()
+    _check(N.load().tns_profile_read(ctx.handle, stage.encode(), C.byref(ms), C.byref(n), C.byref(b)))
+    return ms.value, n.value, b.value
+
+
+def fr_rand_batch(seed: bytes, n: int) -> np.ndarray:
+    """n Fr::rand draws from ChaCha20Rng::from_seed(seed), Montgomery limbs."""
+    out = np.empty((n, 4), dtype=np.uint64)
+    if n:
+        N.load().tns_fr_rand_batch((C.c_uint8 * 32)(*seed), n, N.p64(out))
+    return out
+
+
 def bench_trace(memory_size: int, n_ops: int):
     """Synthetic trace of src/benchmarks.rs:88-99 as SoA arrays (addr, value Montgomery, is_write)."""
     addr = np.empty(n_ops, dtype=np.uint64)

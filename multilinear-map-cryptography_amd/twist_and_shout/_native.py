@@ -94,6 +94,20 @@ SIGNATURES = [
      [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), U64P, U64P, U8P, C.c_size_t, C.POINTER(TnsProof)]),
     ("tns_shout_prove", C.c_int,
      [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), U64P, C.c_size_t, U64P, C.c_size_t, C.POINTER(TnsProof)]),
+    ("tns_buffer_upload", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
+    ("tns_buffer_device_ptr", C.c_void_p, [C.c_void_p]),
+    ("tns_buffer_free", None, [C.c_void_p]),
+    ("tns_twist_prove_device", C.c_int,
+     [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+      C.POINTER(TnsProof)]),
+    ("tns_shout_prove_device", C.c_int,
+     [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+      C.POINTER(TnsProof)]),
+    ("tns_msm_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, U64P]),
+    ("tns_profile_enable", C.c_int, [C.c_void_p, C.c_int]),
+    ("tns_profile_read", C.c_int,
+     [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    ("tns_fr_rand_batch", None, [U8P, C.c_size_t, U64P]),
     ("tns_fr_from_u64", None, [U64P, C.c_size_t, U64P]),
     ("tns_fr_from_canonical", None, [U64P, C.c_size_t, U64P]),
     ("tns_fr_to_canonical", None, [U64P, C.c_size_t, U64P]),

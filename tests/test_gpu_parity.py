@@ -402,7 +402,7 @@ def test_twist_bench_trace_properties(logn):
 
 
 def test_twist_ragged_trace_properties():
-    pp, _ = params(6)
-    addr, val, isw = ts.bench_trace(64, 1000)  # pads to 1024
+    pp, _ = params(8)  # max_operations 1024
+    addr, val, isw = ts.bench_trace(256, 1000)  # pads to 1024
     pr = ts.Twist(pp).prove_soa(addr, val, isw)
     _check_twist_properties(pp, addr, val, isw, pr)
