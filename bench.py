@@ -117,8 +117,8 @@ def cpu_baseline(n_ops):
     from oracle import coracle as co
     from oracle import pyoracle as po
 
-    mem = max(1, n_ops // 4)
-    L = max(0, (mem - 1).bit_length())
+    # C1 shape: setup_params(8), MemoryTrace::new(256), 256 ops (memory size = op count)
+    L = max(0, (n_ops - 1).bit_length())
     cp = co.setup_params(L)
     ops = po.benchmark_trace(1 << L, n_ops)
     t0 = time.perf_counter()
