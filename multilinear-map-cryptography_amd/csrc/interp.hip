@@ -13,175 +13,20 @@
 //     we have  G_{s,2m}(y) = G_{s,m}(y) + y^(m) * G_{s+m,m}(y - m).
 //     y^(m) and the Taylor shift by -m depend only on m, so each level is, for every
 //     block: one Taylor shift (a convolution with the fixed kernel (-m)^k/k!) and one
-//     product with the fixed polynomial y^(m); both use NTTs whose fixed operand is
-//     precomputed per N (InterpPlan) in the transformed domain.
-//
-// NTT: forward = decimation-in-frequency (natural in, bit-reversed out), inverse =
-// decimation-in-time (bit-reversed in, natural out); pointwise products happen in
-// bit-reversed order and the 1/S scaling is folded into the precomputed operands.
-// Levels whose blocks fit a 512-element LDS tile run fused in one kernel; larger
-// levels use LDS passes for the small strides and global radix-2 stages otherwise.
+//     product with the fixed polynomial y^(m); both are cyclic convolutions of size 2m
+//     whose fixed operand is precomputed per N (InterpPlan) in the transformed domain
+//     (ntt.hip: ntt_conv_blocks, 5 HBM passes at 2m = 2^24).
+// Levels whose blocks fit a 512-element LDS tile run fused in one kernel.
 #include <hip/hip_runtime.h>
 
 #include <vector>
 
-#include "common.hpp"
+#include "ntt.hpp"
 
 namespace tns {
 
-// Fr two-adic root of unity of order 2^28 (= 5^((r-1)/2^28); ark-bn254 TWO_ADIC_ROOT_OF_UNITY)
-static Fr root_of_unity_2_28() {
-  // canonical 0x2a3c09f0a58a7e8500e0a7eb8ef62abc402d111e41112ed49bd61b6e725b19f0
-  const uint32_t c[8] = {0x725b19f0u, 0x9bd61b6eu, 0x41112ed4u, 0x402d111eu,
-                         0x8ef62abcu, 0x00e0a7ebu, 0xa58a7e85u, 0x2a3c09f0u};
-  Fr x;
-  for (int i = 0; i < 8; i++) x.v[i] = c[i];
-  return to_mont(x);
-}
+constexpr int INT_TILE_LOG = 9;  // 512-element tiles for the fused interpolation levels
 
-constexpr int NTT_TILE_LOG = 10;  // 1024-element LDS tiles for plain NTT passes
-constexpr int INT_TILE_LOG = 9;   // 512-element tiles for the fused interpolation levels
-
-// ---------------------------------------------------------------- twiddles
-// tw[i] = w^i (i < 2^(L-1)), w a primitive 2^L-th root of unity.
-__global__ void __launch_bounds__(256) k_powers(Fr w, size_t n, Fr *__restrict__ out) {
-  size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  size_t a = j * 64;
-  if (a >= n) return;
-  size_t b = a + 64 < n ? a + 64 : n;
-  Fr p = pow_u64(w, a);
-  for (size_t i = a; i < b; i++) {
-    out[i] = p;
-    p = mul(p, w);
-  }
-}
-
-static void ensure_twiddles(Ctx *c, unsigned L) {
-  if (L < 1) L = 1;
-  if (c->twiddle_log >= L) return;
-  if (L > 28) throw Error(TNS_ERR_POLYNOMIAL, "NTT larger than 2^28 (Fr two-adicity)");
-  Fr w = root_of_unity_2_28();
-  for (unsigned i = L; i < 28; i++) w = sqr(w);
-  size_t n = (size_t)1 << (L - 1);
-  Fr *tw = (Fr *)c->twiddles.ensure(sizeof(Fr) * n);
-  k_powers<<<grid_for((n + 63) / 64, 256, 1u << 30), 256, 0, c->stream>>>(w, n, tw);
-  TNS_LAUNCH_CHECK();
-  c->twiddle_log = L;
-}
-
-// twiddle w_{2h}^k (forward) or w_{2h}^-k (inverse), h = 2^lh
-__device__ __forceinline__ Fr twiddle(const Fr *__restrict__ tw, unsigned lmax, unsigned lh, uint32_t k,
-                                      bool inv_dir) {
-  size_t idx = (size_t)k << (lmax - lh - 1);
-  if (!inv_dir || k == 0) return tw[idx];
-  size_t half = (size_t)1 << (lmax - 1);
-  return neg(tw[half - idx]);  // w^-i = -w^(half - i)
-}
-
-// ---------------------------------------------------------------- LDS NTT building blocks
-// All threads of the block cooperate on `len` elements in LDS holding independent
-// transforms of size 2^(lh_hi+1) laid out contiguously.
-template <bool INV>
-__device__ void lds_ntt(Fr *buf, unsigned len, int lh_hi, const Fr *__restrict__ tw, unsigned lmax) {
-  const unsigned nbf = len >> 1;
-  if (!INV) {
-    for (int lh = lh_hi; lh >= 0; lh--) {
-      const uint32_t h = 1u << lh;
-      for (unsigned q = threadIdx.x; q < nbf; q += blockDim.x) {
-        uint32_t k = q & (h - 1);
-        uint32_t i0 = ((q >> lh) << (lh + 1)) | k, i1 = i0 + h;
-        Fr a = buf[i0], b = buf[i1];
-        buf[i0] = add(a, b);
-        buf[i1] = mul(sub(a, b), twiddle(tw, lmax, lh, k, false));
-      }
-      __syncthreads();
-    }
-  } else {
-    for (int lh = 0; lh <= lh_hi; lh++) {
-      const uint32_t h = 1u << lh;
-      for (unsigned q = threadIdx.x; q < nbf; q += blockDim.x) {
-        uint32_t k = q & (h - 1);
-        uint32_t i0 = ((q >> lh) << (lh + 1)) | k, i1 = i0 + h;
-        Fr a = buf[i0], b = mul(buf[i1], twiddle(tw, lmax, lh, k, true));
-        buf[i0] = add(a, b);
-        buf[i1] = sub(a, b);
-      }
-      __syncthreads();
-    }
-  }
-}
-
-// In-place NTT passes over LDS tiles: stages lh in [0, lh_hi] of transforms of size >= tile.
-template <bool INV>
-__global__ void __launch_bounds__(256) k_ntt_lds(Fr *__restrict__ x, unsigned tile, int lh_hi,
-                                                 const Fr *__restrict__ tw, unsigned lmax) {
-  __shared__ Fr buf[1 << NTT_TILE_LOG];
-  Fr *base = x + (size_t)blockIdx.x * tile;
-  for (unsigned i = threadIdx.x; i < tile; i += blockDim.x) buf[i] = base[i];
-  __syncthreads();
-  lds_ntt<INV>(buf, tile, lh_hi, tw, lmax);
-  for (unsigned i = threadIdx.x; i < tile; i += blockDim.x) base[i] = buf[i];
-}
-
-// One global radix-2 stage (half-size h = 2^lh) over blocks of size 2^s.
-template <bool INV>
-__global__ void __launch_bounds__(256) k_ntt_stage(Fr *__restrict__ x, size_t nbf, unsigned lh,
-                                                   const Fr *__restrict__ tw, unsigned lmax) {
-  for (size_t q = blockIdx.x * (size_t)blockDim.x + threadIdx.x; q < nbf;
-       q += (size_t)gridDim.x * blockDim.x) {
-    const size_t h = (size_t)1 << lh;
-    uint32_t k = (uint32_t)(q & (h - 1));
-    size_t i0 = ((q >> lh) << (lh + 1)) | k, i1 = i0 + h;
-    Fr a = x[i0], b = x[i1];
-    if (!INV) {
-      x[i0] = add(a, b);
-      x[i1] = mul(sub(a, b), twiddle(tw, lmax, lh, k, false));
-    } else {
-      b = mul(b, twiddle(tw, lmax, lh, k, true));
-      x[i0] = add(a, b);
-      x[i1] = sub(a, b);
-    }
-  }
-}
-
-// nb contiguous transforms of size 2^s; forward DIF / inverse DIT (unscaled).
-static void ntt_blocks(Ctx *c, Fr *x, unsigned s, size_t nb, bool inverse) {
-  if (s == 0) return;
-  ensure_twiddles(c, s);
-  const unsigned lmax = c->twiddle_log;
-  const Fr *tw = c->twiddles.as<Fr>();
-  const size_t total = nb << s;
-  const unsigned tile_log = s < NTT_TILE_LOG ? s : NTT_TILE_LOG;
-  // LDS tile covers whole transforms when s <= tile_log, else the low strides
-  size_t tile_len = (size_t)1 << (tile_log);
-  if (total < tile_len) tile_len = total;
-  const int lds_hi = (int)tile_log - 1;  // stages lh <= lds_hi fit inside a tile
-  const size_t ntiles = total / tile_len;
-  const size_t nbf = total >> 1;
-  if (!inverse) {
-    for (int lh = (int)s - 1; lh > lds_hi; lh--) {
-      TNS_PROF(c, "ntt_stage", 64.0 * total);
-      k_ntt_stage<false><<<grid_for(nbf, 256), 256, 0, c->stream>>>(x, nbf, (unsigned)lh, tw, lmax);
-      TNS_LAUNCH_CHECK();
-    }
-    TNS_PROF(c, "ntt_lds", 64.0 * total);
-    k_ntt_lds<false><<<(unsigned)ntiles, 256, 0, c->stream>>>(x, (unsigned)tile_len, lds_hi, tw, lmax);
-    TNS_LAUNCH_CHECK();
-  } else {
-    {
-    TNS_PROF(c, "ntt_lds", 64.0 * total);
-    k_ntt_lds<true><<<(unsigned)ntiles, 256, 0, c->stream>>>(x, (unsigned)tile_len, lds_hi, tw, lmax);
-    TNS_LAUNCH_CHECK();
-    }
-    for (int lh = lds_hi + 1; lh < (int)s; lh++) {
-      TNS_PROF(c, "ntt_stage", 64.0 * total);
-      k_ntt_stage<true><<<grid_for(nbf, 256), 256, 0, c->stream>>>(x, nbf, (unsigned)lh, tw, lmax);
-      TNS_LAUNCH_CHECK();
-    }
-  }
-}
-
-// x[b * S + i] *= w[i]
 __global__ void __launch_bounds__(256) k_pointwise(Fr *__restrict__ x, const Fr *__restrict__ w,
                                                    unsigned s, size_t total) {
   const size_t mask = ((size_t)1 << s) - 1;
@@ -267,7 +112,7 @@ __global__ void __launch_bounds__(256) k_batch_inverse(const Fr *__restrict__ in
   }
 }
 
-// out[t] = sgn^t * c^t * inv_fact[t] for t < n, zero for t in [n, len)
+// out[t] = cst^t * inv_fact[t] for t < n, zero for t in [n, len)
 __global__ void __launch_bounds__(256) k_exp_series(Fr cst, const Fr *__restrict__ inv_fact, size_t n,
                                                     size_t len, Fr *__restrict__ out) {
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < len;
@@ -309,8 +154,7 @@ __global__ void __launch_bounds__(256) k_combine(Fr *__restrict__ A, const Fr *_
 __global__ void __launch_bounds__(256) k_interp_tile(Fr *__restrict__ A, unsigned tile, unsigned levels,
                                                      const Fr *__restrict__ fact,
                                                      const Fr *__restrict__ inv_fact,
-                                                     const Fr *__restrict__ lvl, const Fr *__restrict__ tw,
-                                                     unsigned lmax) {
+                                                     const Fr *__restrict__ lvl, const Fr *__restrict__ TW) {
   __shared__ Fr a[1 << INT_TILE_LOG];
   __shared__ Fr xs[1 << INT_TILE_LOG];
   Fr *g = A + (size_t)blockIdx.x * tile;
@@ -325,10 +169,10 @@ __global__ void __launch_bounds__(256) k_interp_tile(Fr *__restrict__ A, unsigne
       xs[i] = t < m ? mul(a[base + m + (m - 1 - t)], fact[m - 1 - t]) : Fr::zero();
     }
     __syncthreads();
-    lds_ntt<false>(xs, tile, (int)l, tw, lmax);
+    lds_ntt<false>(xs, tile, (int)l, TW);
     for (unsigned i = threadIdx.x; i < tile; i += blockDim.x) xs[i] = mul(xs[i], Vhat[i & (two_m - 1)]);
     __syncthreads();
-    lds_ntt<true>(xs, tile, (int)l, tw, lmax);
+    lds_ntt<true>(xs, tile, (int)l, TW);
     // reversal + 1/i! (read all, then write)
     Fr tmp[(1 << INT_TILE_LOG) / 256];
     {
@@ -344,10 +188,10 @@ __global__ void __launch_bounds__(256) k_interp_tile(Fr *__restrict__ A, unsigne
       for (unsigned i = threadIdx.x; i < tile; i += blockDim.x, q++) xs[i] = tmp[q];
     }
     __syncthreads();
-    lds_ntt<false>(xs, tile, (int)l, tw, lmax);
+    lds_ntt<false>(xs, tile, (int)l, TW);
     for (unsigned i = threadIdx.x; i < tile; i += blockDim.x) xs[i] = mul(xs[i], Phat[i & (two_m - 1)]);
     __syncthreads();
-    lds_ntt<true>(xs, tile, (int)l, tw, lmax);
+    lds_ntt<true>(xs, tile, (int)l, TW);
     for (unsigned i = threadIdx.x; i < tile; i += blockDim.x) {
       unsigned t = i & (two_m - 1);
       a[i] = t < m ? add(xs[i], a[i]) : xs[i];
@@ -363,7 +207,7 @@ __global__ void k_copy_fr(const Fr *__restrict__ in, Fr *__restrict__ out, size_
        i += (size_t)gridDim.x * blockDim.x)
     out[i] = i < n ? in[i] : Fr::zero();
 }
-// out[i] = C(m, i) (-m)^(m-i) = m! / (i! (m-i)!) (-m)^(m-i), i <= m  (binomial part of (y-m)^m)
+// out[i] = C(m, i) (-m)^(m-i), i <= m  (the binomial expansion of (y - m)^m)
 __global__ void k_binom_shift(size_t m, Fr negm, const Fr *__restrict__ fact, const Fr *__restrict__ inv_fact,
                               Fr *__restrict__ out) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i <= m; i += (size_t)gridDim.x * blockDim.x)
@@ -376,6 +220,16 @@ __global__ void k_add_into(Fr *__restrict__ a, const Fr *__restrict__ b, size_t 
 
 static Fr fr_inv_pow2(unsigned s) { return inv(from_u64<FrCfg>((uint64_t)1 << s)); }
 
+// forward transform of `len` coefficients zero-padded to 2^s, scaled by 2^-s (a conv operand)
+static void make_conv_operand(Ctx *c, const Fr *coeffs, size_t len, unsigned s, Fr *out) {
+  const size_t S = (size_t)1 << s;
+  k_copy_fr<<<grid_for(S, 256), 256, 0, c->stream>>>(coeffs, out, len, S);
+  TNS_LAUNCH_CHECK();
+  ntt_blocks(c, out, s, 1, false);
+  k_scale<<<grid_for(S, 256), 256, 0, c->stream>>>(out, fr_inv_pow2(s), S);
+  TNS_LAUNCH_CHECK();
+}
+
 static InterpPlan *get_plan(Ctx *c, unsigned log_n) {
   if (c->plans.size() <= log_n) c->plans.resize(log_n + 1, nullptr);
   if (c->plans[log_n]) return c->plans[log_n];
@@ -383,7 +237,7 @@ static InterpPlan *get_plan(Ctx *c, unsigned log_n) {
   const size_t NF = N < 4 ? 4 : N;  // factorial table length (>= m + 1 for every level)
   InterpPlan *P = new InterpPlan();
   P->log_n = log_n;
-  ensure_twiddles(c, log_n + 2);
+  ntt_twiddles(c, log_n + 2);
   hipStream_t st = c->stream;
   // factorials
   Fr *fact = (Fr *)P->fact.ensure(sizeof(Fr) * NF);
@@ -418,53 +272,36 @@ static InterpPlan *get_plan(Ctx *c, unsigned log_n) {
     Fr *q = (Fr *)q_b.ensure(sizeof(Fr) * 2 * N);
     Fr *t1 = (Fr *)t1_b.ensure(sizeof(Fr) * 2 * N);
     Fr *t2 = (Fr *)t2_b.ensure(sizeof(Fr) * 2 * N);
-    // y^(1) = y
     {
-      Fr h[2] = {Fr::zero(), Fr::one()};
+      Fr h[2] = {Fr::zero(), Fr::one()};  // y^(1) = y
       TNS_HIP(hipMemcpyAsync(pm, h, sizeof h, hipMemcpyHostToDevice, st));
     }
     for (unsigned l = 0; l < log_n; l++) {
       const size_t m = (size_t)1 << l;
       Fr *Vhat = lv + 4 * (m - 1), *Phat = Vhat + 2 * m;
       const Fr negm = neg(from_u64<FrCfg>(m));
-      const Fr scale = fr_inv_pow2(l + 1);
       // Vhat: NTT_{2m}((-m)^k / k!, k < m) / 2m
-      k_exp_series<<<grid_for(2 * m, 256), 256, 0, st>>>(negm, ifact, m, 2 * m, Vhat);
+      k_exp_series<<<grid_for(2 * m, 256), 256, 0, st>>>(negm, ifact, m, 2 * m, t1);
       TNS_LAUNCH_CHECK();
-      ntt_blocks(c, Vhat, l + 1, 1, false);
-      k_scale<<<grid_for(2 * m, 256), 256, 0, st>>>(Vhat, scale, 2 * m);
-      TNS_LAUNCH_CHECK();
+      make_conv_operand(c, t1, 2 * m, l + 1, Vhat);
       // Phat: NTT_{2m}(y^(m)) / 2m  (m+1 coefficients, padded)
-      k_copy_fr<<<grid_for(2 * m, 256), 256, 0, st>>>(pm, Phat, m + 1, 2 * m);
-      TNS_LAUNCH_CHECK();
-      ntt_blocks(c, Phat, l + 1, 1, false);
-      k_scale<<<grid_for(2 * m, 256), 256, 0, st>>>(Phat, scale, 2 * m);
-      TNS_LAUNCH_CHECK();
+      make_conv_operand(c, pm, m + 1, l + 1, Phat);
       if (l + 1 == log_n) break;
-      // y^(2m) = y^(m) * (y - m)^(m);  (y-m)^(m) = (y-m)^m + p(y - m) with p = y^(m) - y^m
-      // Taylor shift of p (m coefficients) by -m: size-4m convolution (generic sizes)
-      const unsigned s4 = l + 2;  // 4m = 2^(l+2)
+      // y^(2m) = y^(m) * (y-m)^(m);  (y-m)^(m) = (y-m)^m + p(y - m) with p = y^(m) - y^m.
+      // Taylor shift of p (m coefficients) by -m as a size-4m convolution.
+      const unsigned s4 = l + 2;
       const size_t L4 = (size_t)4 * m;
-      // t1[t] = p_{m-1-t} (m-1-t)!  for t < m, else 0
-      {
-        // reuse k_build_u on a virtual block: A' = [*, p] -- build explicitly on host-free path
-        k_copy_fr<<<grid_for(L4, 256), 256, 0, st>>>(pm, t2, m, L4);  // t2 = p (coeffs < m)
-        TNS_LAUNCH_CHECK();
-        // t1 = reversed(p) * fact
-        k_build_u<<<grid_for(2 * m, 256), 256, 0, st>>>(t2 - m, t1, m, 2 * m, fact);  // reads t2[0..m)
-        TNS_LAUNCH_CHECK();
-        k_copy_fr<<<grid_for(L4 - 2 * m, 256), 256, 0, st>>>(t1, t1 + 2 * m, 0, L4 - 2 * m);  // zero tail
-        TNS_LAUNCH_CHECK();
-      }
-      ntt_blocks(c, t1, s4, 1, false);
+      k_copy_fr<<<grid_for(L4, 256), 256, 0, st>>>(pm, t2, m, L4);  // t2 = p
+      TNS_LAUNCH_CHECK();
+      k_build_u<<<grid_for(2 * m, 256), 256, 0, st>>>(t2 - m, t1, m, 2 * m, fact);  // t1 = rev(p) * k!
+      TNS_LAUNCH_CHECK();
+      k_copy_fr<<<grid_for(L4 - 2 * m, 256), 256, 0, st>>>(t1, t1 + 2 * m, 0, L4 - 2 * m);  // zero tail
+      TNS_LAUNCH_CHECK();
       k_exp_series<<<grid_for(L4, 256), 256, 0, st>>>(negm, ifact, m, L4, t2);
       TNS_LAUNCH_CHECK();
-      ntt_blocks(c, t2, s4, 1, false);
-      pointwise_blocks(c, t1, t2, s4, 1);
-      ntt_blocks(c, t1, s4, 1, true);
-      k_scale<<<grid_for(L4, 256), 256, 0, st>>>(t1, fr_inv_pow2(s4), L4);
-      TNS_LAUNCH_CHECK();
-      // q[i] = t1[m-1-i] / i!  (i < m) -> p(y - m);  plus binomial part for i <= m
+      make_conv_operand(c, t2, L4, s4, q);  // q: transformed kernel (scratch)
+      ntt_conv_blocks(c, t1, s4, 1, q);
+      // q[i] = t1[m-1-i] / i!  (i < m) -> p(y - m);  plus the binomial part for i <= m
       k_reverse_scale<<<grid_for(2 * m, 256), 256, 0, st>>>(t1, q, m, 2 * m, ifact);
       TNS_LAUNCH_CHECK();
       k_binom_shift<<<grid_for(m + 1, 256), 256, 0, st>>>(m, negm, fact, ifact, t2);
@@ -472,16 +309,10 @@ static InterpPlan *get_plan(Ctx *c, unsigned log_n) {
       k_add_into<<<grid_for(m + 1, 256), 256, 0, st>>>(q, t2, m + 1);
       TNS_LAUNCH_CHECK();
       // y^(2m) = pm * q   (both m+1 coefficients; product 2m+1 <= 4m)
+      make_conv_operand(c, q, m + 1, s4, t2);
       k_copy_fr<<<grid_for(L4, 256), 256, 0, st>>>(pm, t1, m + 1, L4);
       TNS_LAUNCH_CHECK();
-      k_copy_fr<<<grid_for(L4, 256), 256, 0, st>>>(q, t2, m + 1, L4);
-      TNS_LAUNCH_CHECK();
-      ntt_blocks(c, t1, s4, 1, false);
-      ntt_blocks(c, t2, s4, 1, false);
-      pointwise_blocks(c, t1, t2, s4, 1);
-      ntt_blocks(c, t1, s4, 1, true);
-      k_scale<<<grid_for(L4, 256), 256, 0, st>>>(t1, fr_inv_pow2(s4), L4);
-      TNS_LAUNCH_CHECK();
+      ntt_conv_blocks(c, t1, s4, 1, t2);
       k_copy_fr<<<grid_for(2 * m + 1, 256), 256, 0, st>>>(t1, pm, 2 * m + 1, 2 * m + 1);
       TNS_LAUNCH_CHECK();
     }
@@ -509,24 +340,21 @@ void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs) {
   Fr *A = coeffs;
   // 1. Newton coefficients: first n entries of conv(y_j / j!, (-1)^t / t!)
   {
-    // X2[j] = y_j * inv_fact[j] (j < n), 0 above
+    TNS_PROF(c, "interp_elementwise", 64.0 * 2 * n);
     k_copy_fr<<<grid_for(2 * n, 256), 256, 0, st>>>(y, X2, n, 2 * n);
     TNS_LAUNCH_CHECK();
-    pointwise_blocks(c, X2, ifact, log_n, 1);  // first n entries *= 1/j!
-    ntt_blocks(c, X2, log_n + 1, 1, false);
-    pointwise_blocks(c, X2, P->newton_kernel_hat.as<Fr>(), log_n + 1, 1);
-    ntt_blocks(c, X2, log_n + 1, 1, true);
-    TNS_HIP(hipMemcpyAsync(A, X2, sizeof(Fr) * n, hipMemcpyDeviceToDevice, st));
   }
+  pointwise_blocks(c, X2, ifact, log_n, 1);  // first n entries *= 1/j!
+  ntt_conv_blocks(c, X2, log_n + 1, 1, P->newton_kernel_hat.as<Fr>());
+  TNS_HIP(hipMemcpyAsync(A, X2, sizeof(Fr) * n, hipMemcpyDeviceToDevice, st));
   // 2. levels
   const Fr *lv = P->level_tables.as<Fr>();
-  const unsigned lmax = c->twiddle_log;
-  const Fr *tw = c->twiddles.as<Fr>();
+  const Fr *TW = ntt_twiddles(c, log_n + 2);
   const unsigned tile_log = log_n < INT_TILE_LOG ? log_n : INT_TILE_LOG;
   const unsigned tile = 1u << tile_log;
   {
     TNS_PROF(c, "interp_tile", 64.0 * n);
-    k_interp_tile<<<(unsigned)(n / tile), 256, 0, st>>>(A, tile, tile_log, fact, ifact, lv, tw, lmax);
+    k_interp_tile<<<(unsigned)(n / tile), 256, 0, st>>>(A, tile, tile_log, fact, ifact, lv, TW);
     TNS_LAUNCH_CHECK();
   }
   Fr *X = X2, *Y = X2 + n;
@@ -534,18 +362,23 @@ void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs) {
     const size_t m = (size_t)1 << l;
     const size_t nb = n / (2 * m);
     const Fr *Vhat = lv + 4 * (m - 1), *Phat = Vhat + 2 * m;
-    k_build_u<<<grid_for(n, 256), 256, 0, st>>>(A, X, m, n, fact);
-    TNS_LAUNCH_CHECK();
-    ntt_blocks(c, X, l + 1, nb, false);
-    pointwise_blocks(c, X, Vhat, l + 1, nb);
-    ntt_blocks(c, X, l + 1, nb, true);
-    k_reverse_scale<<<grid_for(n, 256), 256, 0, st>>>(X, Y, m, n, ifact);
-    TNS_LAUNCH_CHECK();
-    ntt_blocks(c, Y, l + 1, nb, false);
-    pointwise_blocks(c, Y, Phat, l + 1, nb);
-    ntt_blocks(c, Y, l + 1, nb, true);
-    k_combine<<<grid_for(n, 256), 256, 0, st>>>(A, Y, m, n);
-    TNS_LAUNCH_CHECK();
+    {
+      TNS_PROF(c, "interp_elementwise", 64.0 * n);
+      k_build_u<<<grid_for(n, 256), 256, 0, st>>>(A, X, m, n, fact);
+      TNS_LAUNCH_CHECK();
+    }
+    ntt_conv_blocks(c, X, l + 1, nb, Vhat);  // Taylor shift by -m
+    {
+      TNS_PROF(c, "interp_elementwise", 64.0 * n);
+      k_reverse_scale<<<grid_for(n, 256), 256, 0, st>>>(X, Y, m, n, ifact);
+      TNS_LAUNCH_CHECK();
+    }
+    ntt_conv_blocks(c, Y, l + 1, nb, Phat);  // times y^(m)
+    {
+      TNS_PROF(c, "interp_elementwise", 96.0 * n);
+      k_combine<<<grid_for(n, 256), 256, 0, st>>>(A, Y, m, n);
+      TNS_LAUNCH_CHECK();
+    }
   }
 }
 

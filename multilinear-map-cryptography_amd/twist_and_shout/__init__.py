@@ -703,7 +703,7 @@ def profile_enable(ctx: Context, on: bool = True):
 
 
 PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_reduce", "ntt_stage", "ntt_lds",
-                  "ntt_pointwise", "interp_tile", "sumcheck_round", "open_scan"]
+                  "ntt_pointwise", "interp_tile", "interp_elementwise", "sumcheck_round", "open_scan"]
 
 
 def profile_read(ctx: Context, stage: str):
