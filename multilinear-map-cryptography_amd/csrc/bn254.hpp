@@ -154,7 +154,7 @@ TNS_HD Fp<C> dbl(const Fp<C> &a) {
   return add(a, a);
 }
 
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIPCC__)
 // Device: product-scanning (FIPS) Montgomery multiplication.  Column k accumulates every
 // a_i*b_j and m_i*M_j with i + j = k into a 64-bit register pair with v_mad_u64_u32, whose
 // carry-out (VCC) feeds a 32-bit overflow counter via v_addc_co_u32 -- 2 VALU ops per limb
@@ -170,7 +170,7 @@ TNS_HD Fp<C> dbl(const Fp<C> &a) {
                : "v"(x), "s"(y)                                                                 \
                : "vcc")
 template <class C>
-__device__ __forceinline__ Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
+__device__ __forceinline__ Fp<C> mul_ps_dev(const Fp<C> &a, const Fp<C> &b) {
   u32 m[8], r[8];
   u64 acc = 0;
   u32 c2 = 0;
@@ -202,10 +202,11 @@ __device__ __forceinline__ Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
   reduce_once(o);
   return o;
 }
-#else
-// Host: CIOS Montgomery product, no-carry variant (top modulus limb < 2^31 - 1).
+#endif
+
+// Host (and reference): CIOS Montgomery product, no-carry variant (top modulus limb < 2^31 - 1).
 template <class C>
-inline Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
+TNS_HD Fp<C> mul_cios(const Fp<C> &a, const Fp<C> &b) {
   u32 t[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) t[i] = 0;
@@ -229,7 +230,15 @@ inline Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
   reduce_once(r);
   return r;
 }
+
+template <class C>
+TNS_HD Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return mul_ps_dev(a, b);
+#else
+  return mul_cios(a, b);
 #endif
+}
 
 template <class C>
 TNS_HD Fp<C> sqr(const Fp<C> &a) {
