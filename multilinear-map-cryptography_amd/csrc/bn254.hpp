@@ -160,12 +160,12 @@ TNS_HD Fp<C> dbl(const Fp<C> &a) {
 // carry-out (VCC) feeds a 32-bit overflow counter via v_addc_co_u32 -- 2 VALU ops per limb
 // product instead of the ~4.4 hipcc emits for the CIOS form (tools/mulbench.hip: 1.46x).
 #define TNS_MAC_VV(acc, c2, x, y)                                                               \
-  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"          \
                : "+v"(acc), "+v"(c2)                                                            \
                : "v"(x), "v"(y)                                                                 \
                : "vcc")
 #define TNS_MAC_VS(acc, c2, x, y)                                                               \
-  asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" \
+  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"          \
                : "+v"(acc), "+v"(c2)                                                            \
                : "v"(x), "s"(y)                                                                 \
                : "vcc")
@@ -233,7 +233,7 @@ TNS_HD Fp<C> mul_cios(const Fp<C> &a, const Fp<C> &b) {
 
 template <class C>
 TNS_HD Fp<C> mul(const Fp<C> &a, const Fp<C> &b) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_MUL_CIOS)
   return mul_ps_dev(a, b);
 #else
   return mul_cios(a, b);

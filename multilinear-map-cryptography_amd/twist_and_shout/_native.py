@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_DIR, "libtns.so")
+LIB_PATH = os.environ.get("TNS_LIB") or os.path.join(_PKG_DIR, "libtns.so")  # override: A/B builds
 
 TNS_MAX_ROUNDS = 40
 U64P = C.POINTER(C.c_uint64)
