@@ -39,9 +39,21 @@ static MsmPlan make_plan(size_t n) {
   MsmPlan p;
   int lg = 0;
   while (((size_t)1 << lg) < n) lg++;
-  p.c = lg - 3;
-  if (p.c < 4) p.c = 4;
-  if (p.c > 16) p.c = 16;
+  // window c minimising (bucket adds) W*n + (reduction adds) ~3*W*2^(c-1)
+  auto windows = [](int c) {
+    int W = (254 + c - 1) / c;
+    if (254 - c * (W - 1) > c - 1) W++;
+    return W;
+  };
+  double best = 1e300;
+  p.c = 4;
+  for (int c = 4; c <= 20 && c <= lg + 1; c++) {
+    double cost = (double)windows(c) * (double)n + 3.0 * windows(c) * (double)(1u << (c - 1));
+    if (cost < best * 0.98) {  // prefer the smaller window on near-ties (less bucket memory)
+      best = cost;
+      p.c = c;
+    }
+  }
   p.W = (254 + p.c - 1) / p.c;
   // the top window must not produce a carry: its raw value < 2^(254 - c(W-1)) must be <= 2^(c-1)
   if (254 - p.c * (p.W - 1) > p.c - 1) p.W++;

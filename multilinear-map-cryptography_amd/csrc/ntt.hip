@@ -110,7 +110,7 @@ template <bool INV>
 __global__ void __launch_bounds__(256) k_ntt_pass(Fr *__restrict__ x, size_t ntiles, unsigned lo, unsigned r,
                                                   const Fr *__restrict__ TW) {
   __shared__ Fr buf[(1 << PASS_RMAX) * PASS_COLS];
-  const unsigned rows = 1u << r, elems = rows * PASS_COLS, nbf = elems >> 1;
+  const unsigned rows = 1u << r, elems = rows * PASS_COLS;
   const size_t cgroups = ((size_t)1 << lo) / PASS_COLS;
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t outer = t / cgroups, cg = t % cgroups;
@@ -118,35 +118,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(Fr *__restrict__ x, size_t nti
     for (unsigned e = threadIdx.x; e < elems; e += blockDim.x)
       buf[e] = x[base + ((size_t)(e / PASS_COLS) << lo) + (e % PASS_COLS)];
     __syncthreads();
-    if (!INV) {
-      for (int ll = (int)r - 1; ll >= 0; ll--) {  // local stage ll <-> global lh = lo + ll
-        const unsigned d = 1u << ll;
-        for (unsigned q = threadIdx.x; q < nbf; q += blockDim.x) {
-          const unsigned c = q % PASS_COLS, jj = q / PASS_COLS;
-          const unsigned j0 = ((jj >> ll) << (ll + 1)) | (jj & (d - 1));
-          const uint32_t k = ((j0 & (d - 1)) << lo) + (uint32_t)(cg * PASS_COLS) + c;
-          const unsigned i0 = j0 * PASS_COLS + c, i1 = i0 + d * PASS_COLS;
-          Fr a = buf[i0], b = buf[i1];
-          buf[i0] = add(a, b);
-          buf[i1] = mul(sub(a, b), ntt_tw(TW, lo + ll, k, false));
-        }
-        __syncthreads();
-      }
-    } else {
-      for (unsigned ll = 0; ll < r; ll++) {
-        const unsigned d = 1u << ll;
-        for (unsigned q = threadIdx.x; q < nbf; q += blockDim.x) {
-          const unsigned c = q % PASS_COLS, jj = q / PASS_COLS;
-          const unsigned j0 = ((jj >> ll) << (ll + 1)) | (jj & (d - 1));
-          const uint32_t k = ((j0 & (d - 1)) << lo) + (uint32_t)(cg * PASS_COLS) + c;
-          const unsigned i0 = j0 * PASS_COLS + c, i1 = i0 + d * PASS_COLS;
-          Fr a = buf[i0], b = mul(buf[i1], ntt_tw(TW, lo + ll, k, true));
-          buf[i0] = add(a, b);
-          buf[i1] = sub(a, b);
-        }
-        __syncthreads();
-      }
-    }
+    lds_stages<INV, PASS_COLS>(buf, rows, (int)r - 1, lo, (uint32_t)(cg * PASS_COLS), TW);
     for (unsigned e = threadIdx.x; e < elems; e += blockDim.x)
       x[base + ((size_t)(e / PASS_COLS) << lo) + (e % PASS_COLS)] = buf[e];
     __syncthreads();
