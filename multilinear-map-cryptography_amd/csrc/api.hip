@@ -38,6 +38,7 @@ void set_last_error(const std::string &m) { g_last_error = m; }
 
 Ctx::~Ctx() {
   for (auto *p : plans) delete p;
+  for (auto &kv : pass_tw) delete kv.second;
   if (stream) (void)hipStreamDestroy(stream);
 }
 

@@ -151,6 +151,7 @@ struct Ctx {
   DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
+  std::map<uint32_t, DevBuf *> pass_tw;  // four-step pass twiddles keyed by (lo << 8 | r)
   KernelProfiler prof;
   ~Ctx();
 };

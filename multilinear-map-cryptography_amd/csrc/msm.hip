@@ -193,6 +193,17 @@ __global__ void __launch_bounds__(256) k_bucket_reduce(const G1Xyzz *__restrict_
   }
 }
 
+// out[t] = sum of in[t*chunk .. (t+1)*chunk): shrinks the per-window partial count in
+// parallel before the one-block-per-window tree (windows stay contiguous: chunk | groups).
+__global__ void __launch_bounds__(256) k_sum_chunks(const G1Xyzz *__restrict__ in, size_t n_out, int chunk,
+                                                    G1Xyzz *__restrict__ out) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n_out; t += (size_t)gridDim.x * blockDim.x) {
+    G1Xyzz acc = in[t * chunk];
+    for (int i = 1; i < chunk; i++) acc = xyzz_add(acc, in[t * chunk + i]);
+    out[t] = acc;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_window_sum(const G1Xyzz *__restrict__ parts, int groups,
                                                     G1Xyzz *__restrict__ out) {
   __shared__ G1Xyzz lds[256];
@@ -296,7 +307,18 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
     k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, red_l,
                                                                                   parts);
     TNS_LAUNCH_CHECK();
-    k_window_sum<<<P.W, 256, 0, st>>>(parts, groups, wsum);
+    // shrink groups per window 16x per pass (ping-pong in the bucket array) down to <= 256
+    G1Xyzz *src = parts, *dst = buckets;
+    int g = groups;
+    while (g > 256) {
+      const int chunk = 16;
+      const size_t n_out = (size_t)P.W * (g / chunk);
+      k_sum_chunks<<<grid_for(n_out, 64, 1u << 30), 64, 0, st>>>(src, n_out, chunk, dst);
+      TNS_LAUNCH_CHECK();
+      std::swap(src, dst);
+      g /= chunk;
+    }
+    k_window_sum<<<P.W, 256, 0, st>>>(src, g, wsum);
     TNS_LAUNCH_CHECK();
   }
   std::vector<G1Xyzz> S(P.W);

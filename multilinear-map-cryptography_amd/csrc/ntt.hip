@@ -105,22 +105,70 @@ __global__ void __launch_bounds__(256) k_ntt_tile_conv(Fr *__restrict__ x, unsig
 }
 
 // ---------------------------------------------------------------- strided multi-stage pass
-// Stages lh in [lo, lo + r) on tiles of 2^r rows (2^lo apart) x 8 consecutive columns.
+// Stages lh in [lo, lo + r) of super-blocks of M = 2^(lo+r) elements, on tiles of 2^r rows
+// (2^lo apart) x 8 consecutive columns, in four-step form: the stages' twiddle
+// w_{2h}^{(j mod 2^ll) 2^lo + c} factors into a size-2^r sub-DFT twiddle (tiny table) and
+// a column term that commutes to one multiply per element by w_M^{c rev_r(j)}
+// (forward: after the sub-DFT; inverse: w_M^{-c rev_r(j)} before it).  The per-pass
+// table PT[j 2^lo + c] has the data's own layout, so it streams coalesced with the tile.
+__global__ void __launch_bounds__(256) k_pass_twiddles(const Fr *__restrict__ TW, unsigned lo, unsigned r,
+                                                       Fr *__restrict__ fwd, Fr *__restrict__ inv_) {
+  const size_t M = (size_t)1 << (lo + r), half = M >> 1;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < M; i += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t j = (uint32_t)(i >> lo), c = (uint32_t)(i & (((size_t)1 << lo) - 1));
+    const uint32_t rj = __brev(j) >> (32 - r);
+    const size_t e = (size_t)c * rj;  // < M
+    auto pw = [&](size_t ex) { return ex < half ? TW[half + ex] : neg(TW[ex]); };  // w_M^ex
+    fwd[i] = pw(e);
+    inv_[i] = e ? pw(M - e) : Fr::one();
+  }
+}
+
+static const Fr *pass_table(Ctx *c, unsigned lo, unsigned r) {
+  const uint32_t key = (lo << 8) | r;
+  auto it = c->pass_tw.find(key);
+  if (it != c->pass_tw.end()) return it->second->as<Fr>();
+  const Fr *TW = ntt_twiddles(c, lo + r);
+  const size_t M = (size_t)1 << (lo + r);
+  DevBuf *b = new DevBuf();
+  Fr *t = (Fr *)b->ensure(sizeof(Fr) * 2 * M);
+  k_pass_twiddles<<<grid_for(M, 256), 256, 0, c->stream>>>(TW, lo, r, t, t + M);
+  TNS_LAUNCH_CHECK();
+  c->pass_tw[key] = b;
+  return t;
+}
+
 template <bool INV>
 __global__ void __launch_bounds__(256) k_ntt_pass(Fr *__restrict__ x, size_t ntiles, unsigned lo, unsigned r,
-                                                  const Fr *__restrict__ TW) {
+                                                  const Fr *__restrict__ PT, const Fr *__restrict__ TW) {
   __shared__ Fr buf[(1 << PASS_RMAX) * PASS_COLS];
+  constexpr int PER = ((1 << PASS_RMAX) * PASS_COLS) / 256;
   const unsigned rows = 1u << r, elems = rows * PASS_COLS;
   const size_t cgroups = ((size_t)1 << lo) / PASS_COLS;
   for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     const size_t outer = t / cgroups, cg = t % cgroups;
     const size_t base = (outer << (lo + r)) + cg * PASS_COLS;
-    for (unsigned e = threadIdx.x; e < elems; e += blockDim.x)
-      buf[e] = x[base + ((size_t)(e / PASS_COLS) << lo) + (e % PASS_COLS)];
+    Fr tw[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const unsigned e = threadIdx.x + 256 * q;
+      if (e < elems) {
+        const size_t off = ((size_t)(e / PASS_COLS) << lo) + cg * PASS_COLS + (e % PASS_COLS);
+        tw[q] = PT[off];
+        Fr v = x[(outer << (lo + r)) + off];
+        buf[e] = INV ? mul(v, tw[q]) : v;
+      }
+    }
     __syncthreads();
-    lds_stages<INV, PASS_COLS>(buf, rows, (int)r - 1, lo, (uint32_t)(cg * PASS_COLS), TW);
-    for (unsigned e = threadIdx.x; e < elems; e += blockDim.x)
-      x[base + ((size_t)(e / PASS_COLS) << lo) + (e % PASS_COLS)] = buf[e];
+    lds_stages<INV, PASS_COLS, true>(buf, rows, (int)r - 1, 0, 0, TW);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+      const unsigned e = threadIdx.x + 256 * q;
+      if (e < elems) {
+        Fr v = buf[e];
+        x[base + ((size_t)(e / PASS_COLS) << lo) + (e % PASS_COLS)] = INV ? v : mul(v, tw[q]);
+      }
+    }
     __syncthreads();
   }
 }
@@ -139,13 +187,15 @@ static void strided_passes(Ctx *c, Fr *x, unsigned s, unsigned T, size_t total, 
   }
   if (!inverse) std::reverse(passes.begin(), passes.end());
   for (auto &pr : passes) {
+    const Fr *PT = pass_table(c, pr.first, pr.second);
+    const size_t M = (size_t)1 << (pr.first + pr.second);
     const size_t ntiles = total >> (pr.second + 3);  // 2^r rows x 8 cols per tile
     const unsigned grid = (unsigned)std::min<size_t>(ntiles, 8192);
     TNS_PROF(c, "ntt_stage", 64.0 * total);
     if (!inverse)
-      k_ntt_pass<false><<<grid, 256, 0, c->stream>>>(x, ntiles, pr.first, pr.second, TW);
+      k_ntt_pass<false><<<grid, 256, 0, c->stream>>>(x, ntiles, pr.first, pr.second, PT, TW);
     else
-      k_ntt_pass<true><<<grid, 256, 0, c->stream>>>(x, ntiles, pr.first, pr.second, TW);
+      k_ntt_pass<true><<<grid, 256, 0, c->stream>>>(x, ntiles, pr.first, pr.second, PT + M, TW);
     TNS_LAUNCH_CHECK();
   }
 }

@@ -28,7 +28,9 @@ __device__ __forceinline__ Fr ntt_tw(const Fr *__restrict__ TW, unsigned lh, uin
 // and one barrier per two stages); an odd count does one radix-2 stage first (DIF: the
 // top stage) or last (DIT: the top stage).
 
-template <bool INV, int COLS>
+// SUB = true: a pure size-`rows` sub-DFT per column (twiddle index kl, no column term) --
+// the four-step form used by the strided passes, whose column term is applied separately.
+template <bool INV, int COLS, bool SUB = false>
 __device__ __forceinline__ void lds_radix2(Fr *buf, unsigned rows, int ll, unsigned lo, uint32_t colbase,
                                            const Fr *__restrict__ TW) {
   const unsigned d = 1u << ll, units = (rows >> 1) * COLS;
@@ -36,8 +38,8 @@ __device__ __forceinline__ void lds_radix2(Fr *buf, unsigned rows, int ll, unsig
     const unsigned c = q % COLS, jq = q / COLS;
     const unsigned kl = jq & (d - 1);
     const unsigned j0 = ((jq >> ll) << (ll + 1)) | kl;
-    const uint32_t k = ((uint32_t)kl << lo) + colbase + c;
-    const Fr w = ntt_tw(TW, lo + ll, k, INV);
+    const uint32_t k = SUB ? kl : ((uint32_t)kl << lo) + colbase + c;
+    const Fr w = ntt_tw(TW, SUB ? ll : lo + ll, k, INV);
     const unsigned i0 = j0 * COLS + c, i1 = i0 + d * COLS;
     Fr a = buf[i0], b = buf[i1];
     if (!INV) {
@@ -53,19 +55,20 @@ __device__ __forceinline__ void lds_radix2(Fr *buf, unsigned rows, int ll, unsig
 }
 
 // local stages (ll, ll - 1), quarter distance d = 2^(ll-1)
-template <bool INV, int COLS>
+template <bool INV, int COLS, bool SUB = false>
 __device__ __forceinline__ void lds_radix4(Fr *buf, unsigned rows, int ll, unsigned lo, uint32_t colbase,
                                            const Fr *__restrict__ TW) {
   const unsigned d = 1u << (ll - 1), units = (rows >> 2) * COLS;
+  const unsigned lo_e = SUB ? 0 : lo;
   for (unsigned q = threadIdx.x; q < units; q += blockDim.x) {
     const unsigned c = q % COLS, jq = q / COLS;
     const unsigned kl = jq & (d - 1);
     const unsigned j0 = (jq >> (ll - 1)) * 4 * d + kl;
-    const uint32_t k = ((uint32_t)kl << lo) + colbase + c;
+    const uint32_t k = SUB ? kl : ((uint32_t)kl << lo) + colbase + c;
     // twiddles: stage lh = lo+ll at k and k + d<<lo; stage lh-1 at k
-    const Fr w1 = ntt_tw(TW, lo + ll, k, INV);
-    const Fr w2 = ntt_tw(TW, lo + ll, k + ((uint32_t)d << lo), INV);
-    const Fr w3 = ntt_tw(TW, lo + ll - 1, k, INV);
+    const Fr w1 = ntt_tw(TW, lo_e + ll, k, INV);
+    const Fr w2 = ntt_tw(TW, lo_e + ll, k + ((uint32_t)d << lo_e), INV);
+    const Fr w3 = ntt_tw(TW, lo_e + ll - 1, k, INV);
     const unsigned i0 = j0 * COLS + c, s = d * COLS;
     Fr x0 = buf[i0], x1 = buf[i0 + s], x2 = buf[i0 + 2 * s], x3 = buf[i0 + 3 * s];
     if (!INV) {
@@ -89,21 +92,21 @@ __device__ __forceinline__ void lds_radix4(Fr *buf, unsigned rows, int ll, unsig
 }
 
 // local stages [0, ll_hi] on a rows x COLS tile (DIF high -> low, DIT low -> high)
-template <bool INV, int COLS>
+template <bool INV, int COLS, bool SUB = false>
 __device__ __forceinline__ void lds_stages(Fr *buf, unsigned rows, int ll_hi, unsigned lo, uint32_t colbase,
                                            const Fr *__restrict__ TW) {
   const int n = ll_hi + 1;
   if (!INV) {
     int ll = ll_hi;
     if (n & 1) {
-      lds_radix2<false, COLS>(buf, rows, ll, lo, colbase, TW);
+      lds_radix2<false, COLS, SUB>(buf, rows, ll, lo, colbase, TW);
       ll--;
     }
-    for (; ll >= 1; ll -= 2) lds_radix4<false, COLS>(buf, rows, ll, lo, colbase, TW);
+    for (; ll >= 1; ll -= 2) lds_radix4<false, COLS, SUB>(buf, rows, ll, lo, colbase, TW);
   } else {
     int ll = 1;
-    for (; ll <= ll_hi - (n & 1); ll += 2) lds_radix4<true, COLS>(buf, rows, ll, lo, colbase, TW);
-    if (n & 1) lds_radix2<true, COLS>(buf, rows, ll_hi, lo, colbase, TW);
+    for (; ll <= ll_hi - (n & 1); ll += 2) lds_radix4<true, COLS, SUB>(buf, rows, ll, lo, colbase, TW);
+    if (n & 1) lds_radix2<true, COLS, SUB>(buf, rows, ll_hi, lo, colbase, TW);
   }
 }
 
