@@ -2,9 +2,9 @@
 //
 // A transform of size 2^s over nb contiguous blocks runs as
 //   * strided LDS passes for the large strides: a 256-thread workgroup stages a
-//     2^r x 8 tile (rows 2^lo apart, 8 consecutive columns = 256 contiguous bytes per
-//     row) and runs r <= 7 radix-2 stages in LDS before writing back -- one HBM read
-//     and write per r stages instead of per stage;
+//     2^r x 32 tile (rows 2^lo apart, 32 consecutive columns = 1 KiB contiguous per
+//     row, so each row is a whole DRAM burst run and page) and runs r <= 5 stages in
+//     LDS before writing back -- one HBM read and write per r stages instead of per stage;
 //   * a contiguous 1024-element LDS tile for the 10 smallest strides.
 // ntt_conv_blocks fuses the last forward tile pass, the pointwise product and the
 // first inverse tile pass into one kernel, so a size-2^24 cyclic convolution is
@@ -18,8 +18,8 @@
 namespace tns {
 
 constexpr int TILE_LOG = 10;   // contiguous LDS tile: 1024 Fr = 32 KiB
-constexpr int PASS_COLS = 8;   // columns per strided tile (256 B contiguous)
-constexpr int PASS_RMAX = 7;   // stages per strided pass: 2^7 rows x 8 cols = 1024 Fr
+constexpr int PASS_COLS = 32;  // columns per strided tile: 1 KiB contiguous per row (page/TLB friendly)
+constexpr int PASS_RMAX = 5;   // stages per strided pass: 2^5 rows x 32 cols = 1024 Fr
 
 // Fr two-adic root of unity of order 2^28 (= 5^((r-1)/2^28); ark-bn254 TWO_ADIC_ROOT_OF_UNITY)
 Fr fr_root_of_unity(unsigned log_order) {
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) k_ntt_tile_conv(Fr *__restrict__ x, unsig
 
 // ---------------------------------------------------------------- strided multi-stage pass
 // Stages lh in [lo, lo + r) of super-blocks of M = 2^(lo+r) elements, on tiles of 2^r rows
-// (2^lo apart) x 8 consecutive columns, in four-step form: the stages' twiddle
+// (2^lo apart) x PASS_COLS consecutive columns, in four-step form: the stages' twiddle
 // w_{2h}^{(j mod 2^ll) 2^lo + c} factors into a size-2^r sub-DFT twiddle (tiny table) and
 // a column term that commutes to one multiply per element by w_M^{c rev_r(j)}
 // (forward: after the sub-DFT; inverse: w_M^{-c rev_r(j)} before it).  The per-pass
@@ -189,7 +189,7 @@ static void strided_passes(Ctx *c, Fr *x, unsigned s, unsigned T, size_t total, 
   for (auto &pr : passes) {
     const Fr *PT = pass_table(c, pr.first, pr.second);
     const size_t M = (size_t)1 << (pr.first + pr.second);
-    const size_t ntiles = total >> (pr.second + 3);  // 2^r rows x 8 cols per tile
+    const size_t ntiles = total >> (pr.second + 5);  // 2^r rows x 32 cols per tile
     const unsigned grid = (unsigned)std::min<size_t>(ntiles, 8192);
     TNS_PROF(c, "ntt_stage", 64.0 * total);
     if (!inverse)
