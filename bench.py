@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--log-ops", type=int, default=24, help="Twist trace length 2^k (C4: 24)")
     ap.add_argument("--no-extras", action="store_true", help="skip C2/C3 extras and the CPU baseline")
     ap.add_argument("--cpu-baseline-ops", type=int, default=256, help="oracle sample size (C1: 256)")
+    ap.add_argument("--commit-basis", choices=["lagrange", "coefficients"], default="lagrange",
+                    help="prove via the setup's Lagrange-basis SRS (default) or via interpolation + "
+                         "coefficient KZG (the reference's route); identical proofs")
     return ap.parse_args()
 
 
@@ -140,7 +143,14 @@ def main():
     log_ops = args.log_ops
     n_ops = 1 << log_ops
     L = log_ops - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
+    ctx.set_commit_basis(args.commit_basis == "lagrange")
+    t_setup = time.perf_counter()
     pp, _ = ts.setup_params(L, device=local)
+    t_setup = time.perf_counter() - t_setup
+    t_lag = time.perf_counter()
+    if args.commit_basis == "lagrange":  # setup-time product, like g1_powers (not proving work)
+        pp.commitment_params.srs.prepare_lagrange(n_ops)
+    t_lag = time.perf_counter() - t_lag
     addr, val, isw = ts.bench_trace(1 << L, n_ops)
     d_addr, d_val, d_isw = ts.DeviceBuffer(ctx, addr), ts.DeviceBuffer(ctx, val), ts.DeviceBuffer(ctx, isw)
 
@@ -168,10 +178,14 @@ def main():
         "config": {"workload": f"C4: Twist::prove, 2^{log_ops}-op trace, setup_params({L}), trace resident in HBM",
                    "log_ops": log_ops, "ops_per_gpu": n_ops, "parallelism": f"independent traces x{world}"},
         "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
+        "commit_basis": args.commit_basis,
+        "setup_ms": {"setup_params": round(t_setup * 1e3, 1), "lagrange_basis": round(t_lag * 1e3, 1)},
     }
     if rank == 0 and world == 1 and not args.no_extras:
         # C2: MSM 2^20 pairs (setup_params(18)); scalars = Fr::rand from ChaCha20Rng([7;32])
         pp18, _ = ts.setup_params(18, device=local)
+        if args.commit_basis == "lagrange":
+            pp18.commitment_params.srs.prepare_lagrange(1 << 20)
         n = 1 << 20
         sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
         ts.msm_resident(pp18.commitment_params, sc, n)

@@ -108,6 +108,20 @@ int tns_srs_upload(tns_ctx *ctx, const uint64_t *g1_affine, size_t n, tns_srs **
 int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_affine_out, size_t n);
 size_t tns_srs_len(const tns_srs *srs);
 void tns_srs_destroy(tns_srs *srs);
+/* Attach the setup trapdoor kept in CommitmentParams.tau (src/utils.rs:60-61, :94-100)
+ * to an uploaded SRS (tns_setup_params attaches it itself).  With it the SRS also
+ * provides the Lagrange basis [L_j(tau)]G of the nodes {0..N-1}, which lets
+ * Twist/Shout::prove commit to and open evaluation vectors without interpolating
+ * them (same commitments and proofs).  tau: Montgomery-form Fr. */
+int tns_srs_set_tau(tns_srs *srs, const uint64_t tau[4]);
+/* Build (and cache in the SRS) the Lagrange basis for N = 2^k nodes ahead of the first
+ * proof of that size; part of setup, not of proving.  TNS_ERR_INVALID_PARAMETERS when
+ * the SRS has no tau or N is not a power of two. */
+int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n);
+/* Prove path selection: lagrange != 0 (default) commits/opens through the Lagrange
+ * basis when the SRS has tau; 0 forces vector_to_polynomial + coefficient KZG
+ * (src/twist.rs:151-163).  Both produce identical proofs. */
+int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange);
 
 /* ---------------------------------------------------------------- KZG (src/commitments.rs) */
 /* CommitmentScheme::commit for KZGCommitment (src/commitments.rs:162-180).
@@ -118,6 +132,14 @@ int tns_kzg_commit(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, siz
  * :305-313) and proof = commit((P - v) / (x - z)) (:317-375). n <= 1 -> identity proof. */
 int tns_kzg_open(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, size_t n,
                  const uint64_t z[4], uint64_t value[4], uint64_t proof_proj[12]);
+/* commit(vector_to_polynomial(evals)) and open(vector_to_polynomial(evals), z) in one
+ * step (src/polynomials.rs:248-262 then src/commitments.rs:162-199), as Twist/Shout::prove
+ * do: through the SRS's Lagrange basis when it has tau, else by interpolation.  n must
+ * be a power of two (the provers pad to one, src/twist.rs:141). */
+int tns_kzg_commit_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n,
+                         uint64_t out_proj[12]);
+int tns_kzg_open_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n,
+                       const uint64_t z[4], uint64_t value[4], uint64_t proof_proj[12]);
 /* KZGCommitmentValue::hash (src/commitments.rs:73-84).  Host only. */
 int tns_commitment_hash(const uint64_t proj[12], uint64_t out[4]);
 /* Raw MSM: sum_i scalars[i] * points[i] over the first n SRS points. */

@@ -102,6 +102,42 @@ static void open_dev(Ctx *c, const Srs &srs, const Fr *coeffs, size_t n, const F
   *proof = commit_dev(c, srs, s + 1, n - 1);
 }
 
+// One committed vector of Twist/Shout::prove: evaluations y on the nodes 0..N-1
+// (vector_to_polynomial input, src/polynomials.rs:248-262).  Committed and opened via
+// the Lagrange basis when the SRS provides it, else via interpolated coefficients.
+struct EvalPoly {
+  const Fr *y = nullptr;       // device, N (must stay intact until opened)
+  Fr *coeffs = nullptr;        // device scratch, N (coefficient path)
+  size_t N = 0;
+  const G1Affine *basis = nullptr;
+  bool have_coeffs = false;
+};
+
+static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p) {
+  if (p.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+  p.basis = lagrange_basis_dev(c, srs, p.N);
+  if (p.basis) return xyzz_to_affine(msm_dev(c, p.basis, p.y, p.N));
+  interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
+  p.have_coeffs = true;
+  return commit_dev(c, srs, p.coeffs, p.N);
+}
+
+static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *value, G1Affine *proof,
+                       DevBuf &sbuf) {
+  if (p.basis) {
+    Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.N);
+    if (lagrange_quotient_dev(c, p.y, p.N, z, value, q)) {
+      *proof = xyzz_to_affine(msm_dev(c, p.basis, q, p.N));
+      return;
+    }
+  }
+  if (!p.have_coeffs) {  // z is a node (or no basis): coefficient form
+    interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
+    p.have_coeffs = true;
+  }
+  open_dev(c, srs, p.coeffs, p.N, z, value, proof, sbuf);
+}
+
 // multi-threaded element-wise host conversion
 template <class C, class F>
 static void par_convert(const uint64_t *in, size_t n, uint64_t *out, F f) {
@@ -186,6 +222,8 @@ int tns_setup_params(tns_ctx *ctx, unsigned log_size, tns_params *out, tns_srs *
       tns_srs *s = new tns_srs();
       s->s.device = ctx->c.device;
       s->s.n = out->num_powers;
+      s->s.has_tau = true;
+      s->s.tau = tau;
       try {
         G1Affine *pts = (G1Affine *)s->s.points.ensure(sizeof(G1Affine) * s->s.n);
         srs_generate_dev(&ctx->c, tau, s->s.n, pts);
@@ -227,6 +265,41 @@ int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_out, size_t 
 }
 
 size_t tns_srs_len(const tns_srs *srs) { return srs ? srs->s.n : 0; }
+
+int tns_srs_set_tau(tns_srs *srs, const uint64_t tau[4]) {
+  return guarded([&]() {
+    if (!srs) throw Error(TNS_ERR_INVALID_PARAMETERS, "null SRS");
+    Fr t;
+    std::memcpy(&t, tau, 32);
+    for (auto &kv : srs->s.lagrange) delete kv.second;
+    srs->s.lagrange.clear();
+    srs->s.tau = t;
+    srs->s.has_tau = true;
+    return TNS_OK;
+  });
+}
+
+int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    if (!srs->s.has_tau) throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS has no tau");
+    if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
+    const bool saved = ctx->c.lagrange_commit;
+    ctx->c.lagrange_commit = true;
+    const G1Affine *b = lagrange_basis_dev(&ctx->c, srs->s, n);
+    ctx->c.lagrange_commit = saved;
+    (void)b;  // nullptr only when tau is itself a node: the coefficient path is used then
+    return TNS_OK;
+  });
+}
+
+int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.lagrange_commit = lagrange != 0;
+    return TNS_OK;
+  });
+}
 void tns_srs_destroy(tns_srs *srs) {
   if (!srs) return;
   (void)hipSetDevice(srs->s.device);
@@ -241,6 +314,45 @@ int tns_kzg_commit(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, siz
     Fr *dc = (Fr *)d.ensure(sizeof(Fr) * (n ? n : 1));
     if (n) TNS_HIP(hipMemcpyAsync(dc, coeffs, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
     store_proj(commit_dev(&ctx->c, srs->s, dc, n), out);
+    return TNS_OK;
+  });
+}
+
+static void upload_evals(tns_ctx *ctx, const uint64_t *evals, size_t n, DevBuf &d, DevBuf &cf, EvalPoly &p) {
+  if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_POLYNOMIAL, "evaluation vector length must be a power of two");
+  Fr *dy = (Fr *)d.ensure(sizeof(Fr) * n);
+  TNS_HIP(hipMemcpyAsync(dy, evals, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
+  p.y = dy;
+  p.N = n;
+  p.coeffs = (Fr *)cf.ensure(sizeof(Fr) * n);
+}
+
+int tns_kzg_commit_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n, uint64_t out[12]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    DevBuf d, cf;
+    EvalPoly p;
+    upload_evals(ctx, evals, n, d, cf, p);
+    store_proj(commit_evals(&ctx->c, srs->s, p), out);
+    return TNS_OK;
+  });
+}
+
+int tns_kzg_open_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n, const uint64_t z[4],
+                       uint64_t value[4], uint64_t proof[12]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    DevBuf d, cf, s;
+    EvalPoly p;
+    upload_evals(ctx, evals, n, d, cf, p);
+    if (n > srs->s.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+    p.basis = lagrange_basis_dev(&ctx->c, srs->s, n);
+    Fr zz, v;
+    std::memcpy(&zz, z, 32);
+    G1Affine pi;
+    open_evals(&ctx->c, srs->s, p, zz, &v, &pi, s);
+    std::memcpy(value, &v, 32);
+    store_proj(pi, proof);
     return TNS_OK;
   });
 }
@@ -390,8 +502,8 @@ int tns_last_prove_timing(tns_ctx *ctx, double out_ms[6]) {
 
 // ---------------------------------------------------------------- protocols
 static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *const *mles, int n_mles,
-                             unsigned nv, const Fr *polyA, size_t nA, const Fr *polyB, size_t nB,
-                             tns_proof *out, double *timing, DevBuf &sbuf) {
+                             unsigned nv, EvalPoly &polyA, EvalPoly &polyB, tns_proof *out, double *timing,
+                             DevBuf &sbuf) {
   Timer t_sc;
   std::vector<Fr> rounds(4 * (size_t)(nv ? nv : 1)), chal(nv ? nv : 1);
   Fr finals[4], fe;
@@ -415,8 +527,8 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     std::memcpy(out->opening_point, &z, 32);
     Fr va, vb;
     G1Affine pa, pb;
-    open_dev(c, srs, polyA, nA, z, &va, &pa, sbuf);
-    open_dev(c, srs, polyB, nB, z, &vb, &pb, sbuf);
+    open_evals(c, srs, polyA, z, &va, &pa, sbuf);
+    open_evals(c, srs, polyB, z, &vb, &pb, sbuf);
     store_proj(pa, out->opening_proofs[0]);
     store_proj(pb, out->opening_proofs[1]);
     std::memcpy(out->final_evaluations[0], &va, 32);
@@ -479,17 +591,22 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
-  // ---- vector_to_polynomial x2 (src/twist.rs:151-152)
+  // ---- vector_to_polynomial + commit x2 (src/twist.rs:151-163).  The sum-check below
+  // folds A and V in place, so the openings work from copies of the evaluations.
   Timer t_int;
-  Fr *CA = (Fr *)d_ca.ensure(sizeof(Fr) * N), *CV = (Fr *)d_cv.ensure(sizeof(Fr) * N);
-  interpolate_consecutive_dev(c, A, N, CA);
-  interpolate_consecutive_dev(c, V, N, CV);
-  TNS_HIP(hipStreamSynchronize(st));
+  EvalPoly pa, pv;
+  pa.N = pv.N = N;
+  pa.coeffs = (Fr *)d_ca.ensure(sizeof(Fr) * N);
+  pv.coeffs = (Fr *)d_cv.ensure(sizeof(Fr) * N);
+  Fr *YA = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * N), *YV = (Fr *)c->prove_ws[9].ensure(sizeof(Fr) * N);
+  TNS_HIP(hipMemcpyAsync(YA, A, sizeof(Fr) * N, hipMemcpyDeviceToDevice, st));
+  TNS_HIP(hipMemcpyAsync(YV, V, sizeof(Fr) * N, hipMemcpyDeviceToDevice, st));
+  pa.y = YA;
+  pv.y = YV;
   tm[1] = t_int.ms();
-  // ---- commit x2 (src/twist.rs:155-163)
   Timer t_com;
-  G1Affine Ca = commit_dev(c, srs->s, CA, N);
-  G1Affine Cv = commit_dev(c, srs->s, CV, N);
+  G1Affine Ca = commit_evals(c, srs->s, pa);
+  G1Affine Cv = commit_evals(c, srs->s, pv);
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
   tm[2] = t_com.ms();
@@ -501,7 +618,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tr.append_fr(commitment_hash(Cv));
   // ---- sum-check over the addr / value / op-type MLEs + openings (src/twist.rs:177-243)
   Fr *mles[3] = {A, V, O};
-  fill_common_tail(c, srs->s, tr, mles, 3, nv, CA, N, CV, N, out, tm, d_s);
+  fill_common_tail(c, srs->s, tr, mles, 3, nv, pa, pv, out, tm, d_s);
   TNS_HIP(hipStreamSynchronize(st));
   tm[5] = total.ms();
 }
@@ -566,14 +683,19 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   Timer t_int;
-  Fr *CT = (Fr *)d_ct.ensure(sizeof(Fr) * T), *CI = (Fr *)d_ci.ensure(sizeof(Fr) * M);
-  interpolate_consecutive_dev(c, TB, T, CT);
-  interpolate_consecutive_dev(c, I, M, CI);
-  TNS_HIP(hipStreamSynchronize(st));
+  EvalPoly pt, pi;
+  pt.N = T;
+  pi.N = M;
+  pt.coeffs = (Fr *)d_ct.ensure(sizeof(Fr) * T);
+  pi.coeffs = (Fr *)d_ci.ensure(sizeof(Fr) * M);
+  Fr *YI = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * M);  // the sum-check folds I in place
+  TNS_HIP(hipMemcpyAsync(YI, I, sizeof(Fr) * M, hipMemcpyDeviceToDevice, st));
+  pt.y = TB;
+  pi.y = YI;
   tm[1] = t_int.ms();
   Timer t_com;
-  G1Affine Ct = commit_dev(c, srs->s, CT, T);  // table first (src/shout.rs:125-133)
-  G1Affine Ci = commit_dev(c, srs->s, CI, M);
+  G1Affine Ct = commit_evals(c, srs->s, pt);  // table first (src/shout.rs:125-133)
+  G1Affine Ci = commit_evals(c, srs->s, pi);
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);
   tm[2] = t_com.ms();
@@ -583,7 +705,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tr.append_label("index_commitment");
   tr.append_fr(commitment_hash(Ci));
   Fr *mles[1] = {I};  // the closure evaluates only the index MLE (src/shout.rs:175)
-  fill_common_tail(c, srs->s, tr, mles, 1, nv, CT, T, CI, M, out, tm, d_s);
+  fill_common_tail(c, srs->s, tr, mles, 1, nv, pt, pi, out, tm, d_s);
   TNS_HIP(hipStreamSynchronize(st));
   tm[5] = total.ms();
 }

@@ -82,6 +82,17 @@ struct Srs {
   DevBuf points;  // G1Affine[n]
   size_t n = 0;
   int device = 0;
+  // setup_params keeps tau in CommitmentParams (src/utils.rs:94-100); with it the setup
+  // also yields the Lagrange basis of the nodes {0..N-1}: G * L_j(tau) (lagrange.hip).
+  bool has_tau = false;
+  Fr tau;
+  mutable std::map<unsigned, DevBuf *> lagrange;  // log N -> G1Affine[N] (cache)
+  Srs() = default;
+  Srs(const Srs &) = delete;
+  Srs &operator=(const Srs &) = delete;
+  ~Srs() {
+    for (auto &kv : lagrange) delete kv.second;
+  }
 };
 
 // Per-kernel device time from HIP events recorded on the context stream around
@@ -147,11 +158,14 @@ struct Ctx {
   // workspaces
   DevBuf scratch[8];
   DevBuf msm_ws[10];
+  DevBuf fix_ws;        // MSM heavy-bucket level sums
   DevBuf prove_ws[12];  // resident trace / coefficient vectors of Twist/Shout::prove
   DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
   std::map<uint32_t, DevBuf *> pass_tw;  // four-step pass twiddles keyed by (lo << 8 | r)
+  std::map<unsigned, DevBuf *> bary_w;   // log N -> barycentric weights of nodes {0..N-1}
+  bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
   KernelProfiler prof;
   ~Ctx();
 };
@@ -215,6 +229,18 @@ G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n);
 
 // interp.hip
 void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs);
+void factorial_tables_dev(Ctx *c, size_t nf, Fr *fact, Fr *ifact);
+
+// poly.hip: out[i] = G * s_i (affine), scalars canonical
+void fixed_base_mul_dev(Ctx *c, const Fr *scalars_canon, size_t n, G1Affine *out);
+
+// lagrange.hip: KZG on evaluations over the nodes {0..N-1}
+// Lagrange basis G * L_j(tau) for N (cached in srs); nullptr when srs has no tau or
+// tau is itself a node.
+const G1Affine *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N);
+// v = P(z) and q(j) = (P(j) - v) / (j - z) on the nodes (q: device, N), for z not a
+// node; returns false (nothing written) when z is a node.
+bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q);
 
 // host-side helpers (transcript.cpp)
 struct HostTranscript {

@@ -218,6 +218,22 @@ __global__ void k_add_into(Fr *__restrict__ a, const Fr *__restrict__ b, size_t 
     a[i] = add(a[i], b[i]);
 }
 
+// fact[k] = k!, ifact[k] = 1/k! for k < nf (device; synchronises the stream)
+void factorial_tables_dev(Ctx *c, size_t nf, Fr *fact, Fr *ifact) {
+  hipStream_t st = c->stream;
+  DevBuf iota, pre;
+  Fr *io = (Fr *)iota.ensure(sizeof(Fr) * nf);
+  k_iota_fr<<<grid_for(nf, 256), 256, 0, st>>>(io, nf);
+  TNS_LAUNCH_CHECK();
+  std::vector<DevBuf *> tmp;
+  prefix_product(c, io, nf, fact, tmp);
+  Fr *pr = (Fr *)pre.ensure(sizeof(Fr) * nf);
+  k_batch_inverse<<<grid_for((nf + 31) / 32, 256, 1u << 30), 256, 0, st>>>(fact, nf, pr, ifact);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipStreamSynchronize(st));
+  for (auto *b : tmp) delete b;
+}
+
 static Fr fr_inv_pow2(unsigned s) { return inv(from_u64<FrCfg>((uint64_t)1 << s)); }
 
 // forward transform of `len` coefficients zero-padded to 2^s, scaled by 2^-s (a conv operand)
@@ -242,19 +258,7 @@ static InterpPlan *get_plan(Ctx *c, unsigned log_n) {
   // factorials
   Fr *fact = (Fr *)P->fact.ensure(sizeof(Fr) * NF);
   Fr *ifact = (Fr *)P->inv_fact.ensure(sizeof(Fr) * NF);
-  {
-    DevBuf iota, pre;
-    Fr *io = (Fr *)iota.ensure(sizeof(Fr) * NF);
-    k_iota_fr<<<grid_for(NF, 256), 256, 0, st>>>(io, NF);
-    TNS_LAUNCH_CHECK();
-    std::vector<DevBuf *> tmp;
-    prefix_product(c, io, NF, fact, tmp);
-    Fr *pr = (Fr *)pre.ensure(sizeof(Fr) * NF);
-    k_batch_inverse<<<grid_for((NF + 31) / 32, 256, 1u << 30), 256, 0, st>>>(fact, NF, pr, ifact);
-    TNS_LAUNCH_CHECK();
-    TNS_HIP(hipStreamSynchronize(st));
-    for (auto *b : tmp) delete b;
-  }
+  factorial_tables_dev(c, NF, fact, ifact);
   // Newton kernel: NTT_{2N}((-1)^t / t!) / (2N)
   {
     Fr *wh = (Fr *)P->newton_kernel_hat.ensure(sizeof(Fr) * 2 * N);

@@ -1,0 +1,219 @@
+// lagrange.hip -- KZG commit/open directly on evaluations over the nodes {0..N-1}.
+//
+// The reference commits to vector_to_polynomial(v) (src/polynomials.rs:248-262): the
+// coefficients of the interpolant of v on the nodes 0..N-1, then C = sum_i c_i tau^i G
+// (src/commitments.rs:162-180), and opens with P(z) and the commitment to
+// (P(x) - P(z)) / (x - z) (src/commitments.rs:182-199).  Both group elements are
+// values of polynomials at tau, so with the Lagrange basis of those nodes
+//     L_j(tau) = ell(tau) * w_j / (tau - j),  ell(x) = prod_k (x - k),
+//     w_j = 1 / prod_{k != j} (j - k) = (-1)^(N-1-j) / (j! (N-1-j)!)
+// they are the same points computed without the coefficient form:
+//     commit:  C  = sum_j v_j * [L_j(tau)] G
+//     open:    P(z) = ell(z) * sum_j w_j v_j / (z - j)        (barycentric form)
+//              pi = sum_j q_j [L_j(tau)] G,  q_j = (P(z) - v_j) / (z - j)
+// (q has degree N - 2, so its values on the N nodes determine it exactly).  The basis
+// [L_j(tau)] G is derived once per N from the setup's tau -- the same trusted-setup
+// output as the powers g1_powers, like the Lagrange-form SRS of production KZG
+// ceremonies -- and cached with the SRS.  Each proof is then O(N) field work plus the
+// MSMs; the interpolation (interp.hip) stays the path for SRSs without tau and for the
+// probability-2^-230 case of a challenge that lands on a node.
+//
+// One O(N) building block serves both: inverses of (x - j) for all nodes by a batch
+// inversion whose per-thread chains stride the array (coalesced), with ell(x) as the
+// product of the chain products.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "common.hpp"
+
+namespace tns {
+
+constexpr unsigned NODE_THREADS = 512 * 256;  // batch-inversion chains (one Fermat inverse each)
+
+// chain t: elements i = t + k*T.  pre[i] = prod of earlier (x - i') of the chain; cp[t] = chain product
+__global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr Tm, Fr *__restrict__ pre,
+                                                    Fr *__restrict__ cp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)t));  // x - i, stepping by -T
+  Fr acc = Fr::one();
+  for (size_t i = t; i < n; i += T) {
+    pre[i] = acc;
+    acc = mul(acc, d);
+    d = sub(d, Tm);
+  }
+  cp[t] = acc;
+}
+
+// out[0] = prod_i in[i] (one block)
+__global__ void __launch_bounds__(1024) k_prod_reduce(const Fr *__restrict__ in, size_t n, Fr *__restrict__ out) {
+  __shared__ Fr lds[1024];
+  Fr acc = Fr::one();
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = mul(acc, in[i]);
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) lds[threadIdx.x] = mul(lds[threadIdx.x], lds[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = lds[0];
+}
+
+// out[0] = scale[0] * sum_i in[i] (one block)
+__global__ void __launch_bounds__(1024) k_sum_reduce_scaled(const Fr *__restrict__ in, size_t n,
+                                                            const Fr *__restrict__ scale, Fr *__restrict__ out) {
+  __shared__ Fr lds[1024];
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = add(acc, in[i]);
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) lds[threadIdx.x] = add(lds[threadIdx.x], lds[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = mul(lds[0], scale[0]);
+}
+
+// Backward sweep of chain t: inv_i = 1/(x - i) from pre[i] and the chain inverse.
+//   BASIS: out[i] = canonical(ell * w_i * inv_i)            (Lagrange scalars L_i(x))
+//   OPEN:  out[i] = inv_i, sp[t] = sum_chain w_i y_i inv_i  (barycentric partial sum)
+template <bool BASIS>
+// (pre and out may alias: each element's pre is read before its output is written)
+__global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
+                                                     const Fr *__restrict__ cp, const Fr *__restrict__ w,
+                                                     const Fr *__restrict__ y, const Fr *__restrict__ ell,
+                                                     Fr *out, Fr *__restrict__ sp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  if (t >= n) {
+    if (!BASIS) sp[t] = Fr::zero();
+    return;
+  }
+  const size_t cnt = (n - 1 - t) / T;  // index of the chain's last element
+  size_t i = t + cnt * T;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
+  Fr iv = inv(cp[t]);
+  Fr s = Fr::zero();
+  const Fr L = BASIS ? ell[0] : Fr::one();
+  for (;;) {
+    const Fr inv_i = mul(iv, pre[i]);
+    iv = mul(iv, d);
+    if (BASIS) {
+      out[i] = from_mont(mul(mul(L, w[i]), inv_i));
+    } else {
+      out[i] = inv_i;
+      s = add(s, mul(mul(w[i], y[i]), inv_i));
+    }
+    if (i < T) break;
+    i -= T;
+    d = add(d, Tm);
+  }
+  if (!BASIS) sp[t] = s;
+}
+
+// q_i = (v - y_i) * inv_i, in place over inv
+__global__ void __launch_bounds__(256) k_node_quotient(const Fr *__restrict__ y, const Fr *__restrict__ v,
+                                                       size_t n, Fr *__restrict__ q) {
+  const Fr vv = v[0];
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    q[i] = mul(sub(vv, y[i]), q[i]);
+}
+
+// w_j = (-1)^(N-1-j) / (j! (N-1-j)!)
+__global__ void __launch_bounds__(256) k_bary_weights(const Fr *__restrict__ ifact, size_t n, Fr *__restrict__ w) {
+  for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x) {
+    Fr x = mul(ifact[j], ifact[n - 1 - j]);
+    w[j] = ((n - 1 - j) & 1) ? neg(x) : x;
+  }
+}
+
+static const Fr *bary_weights(Ctx *c, size_t N) {
+  const unsigned lg = ilog2_exact(N);
+  auto it = c->bary_w.find(lg);
+  if (it != c->bary_w.end()) return it->second->as<Fr>();
+  DevBuf fact, ifact;
+  Fr *f = (Fr *)fact.ensure(sizeof(Fr) * N), *fi = (Fr *)ifact.ensure(sizeof(Fr) * N);
+  factorial_tables_dev(c, N, f, fi);
+  DevBuf *b = new DevBuf();
+  Fr *w = (Fr *)b->ensure(sizeof(Fr) * N);
+  k_bary_weights<<<grid_for(N, 256), 256, 0, c->stream>>>(fi, N, w);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipStreamSynchronize(c->stream));  // fact/ifact die here
+  c->bary_w[lg] = b;
+  return w;
+}
+
+// x (Montgomery) equals one of the nodes 0..N-1?
+static bool is_node(const Fr &x, size_t N) {
+  Fr k = from_mont(x);
+  for (int i = 2; i < 8; i++)
+    if (k.v[i]) return false;
+  const uint64_t v = (uint64_t)k.v[0] | ((uint64_t)k.v[1] << 32);
+  return v < N;
+}
+
+struct NodeSweep {
+  size_t T;
+  Fr Tm;
+  Fr *cp, *sp, *dev;  // chain products, partial sums, device scalars (ell, v)
+};
+
+static NodeSweep node_sweep_begin(Ctx *c, const Fr &x, size_t N, Fr *pre) {
+  NodeSweep s;
+  s.T = N < NODE_THREADS ? N : NODE_THREADS;
+  s.Tm = from_u64<FrCfg>((uint64_t)s.T);
+  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (2 * s.T + 4));
+  s.cp = ws;
+  s.sp = ws + s.T;
+  s.dev = ws + 2 * s.T;
+  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(x, N, s.T, s.Tm, pre, s.cp);
+  TNS_LAUNCH_CHECK();
+  k_prod_reduce<<<1, 1024, 0, c->stream>>>(s.cp, s.T, s.dev);  // ell(x)
+  TNS_LAUNCH_CHECK();
+  return s;
+}
+
+const G1Affine *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N) {
+  if (!c->lagrange_commit || !srs.has_tau || N == 0 || (N & (N - 1))) return nullptr;
+  if (is_node(srs.tau, N)) return nullptr;
+  const unsigned lg = ilog2_exact(N);
+  auto it = srs.lagrange.find(lg);
+  if (it != srs.lagrange.end()) return it->second->as<G1Affine>();
+  const Fr *w = bary_weights(c, N);
+  DevBuf scal;
+  Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * N);  // pre, then canonical L_j(tau) in place
+  NodeSweep s = node_sweep_begin(c, srs.tau, N, sc);
+  k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(srs.tau, N, s.T, s.Tm, sc, s.cp, w,
+                                                                           nullptr, s.dev, sc, nullptr);
+  TNS_LAUNCH_CHECK();
+  DevBuf *b = new DevBuf();
+  try {
+    G1Affine *pts = (G1Affine *)b->ensure(sizeof(G1Affine) * N);
+    fixed_base_mul_dev(c, sc, N, pts);  // synchronises
+  } catch (...) {
+    delete b;
+    throw;
+  }
+  srs.lagrange[lg] = b;
+  return b->as<G1Affine>();
+}
+
+bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q) {
+  if (N == 0 || is_node(z, N)) return false;
+  TNS_PROF(c, "open_scan", 32.0 * 6 * N);  // q: pre write/read, inv write/read, y twice
+  const Fr *w = bary_weights(c, N);
+  NodeSweep s = node_sweep_begin(c, z, N, q);
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(z, N, s.T, s.Tm, q, s.cp, w, y,
+                                                                            nullptr, q, s.sp);
+  TNS_LAUNCH_CHECK();
+  k_sum_reduce_scaled<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev, s.dev + 1);  // v = ell(z) * sum
+  TNS_LAUNCH_CHECK();
+  k_node_quotient<<<grid_for(N, 256), 256, 0, c->stream>>>(y, s.dev + 1, N, q);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipMemcpyAsync(value, s.dev + 1, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  return true;
+}
+
+}  // namespace tns

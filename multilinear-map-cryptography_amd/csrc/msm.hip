@@ -35,16 +35,19 @@ struct MsmPlan {
   size_t nb;  // W * 2^(c-1)
 };
 
-static MsmPlan make_plan(size_t n) {
+// bits: bit length of the largest scalar (the windows above it are all zero; commitments
+// to traces -- addresses, small values, flags -- often have bits << 254)
+static MsmPlan make_plan(size_t n, int bits) {
   MsmPlan p;
   int lg = 0;
   while (((size_t)1 << lg) < n) lg++;
-  // window c minimising (bucket adds) W*n + (reduction adds) ~3*W*2^(c-1)
-  auto windows = [](int c) {
-    int W = (254 + c - 1) / c;
-    if (254 - c * (W - 1) > c - 1) W++;
+  // the top window must not produce a carry: its raw value < 2^(bits - c(W-1)) must be <= 2^(c-1)
+  auto windows = [bits](int c) {
+    int W = (bits + c - 1) / c;
+    if (bits - c * (W - 1) > c - 1) W++;
     return W;
   };
+  // window c minimising (bucket adds) W*n + (reduction adds) ~3*W*2^(c-1)
   double best = 1e300;
   p.c = 4;
   for (int c = 4; c <= 20 && c <= lg + 1; c++) {
@@ -54,15 +57,33 @@ static MsmPlan make_plan(size_t n) {
       p.c = c;
     }
   }
-  p.W = (254 + p.c - 1) / p.c;
-  // the top window must not produce a carry: its raw value < 2^(254 - c(W-1)) must be <= 2^(c-1)
-  if (254 - p.c * (p.W - 1) > p.c - 1) p.W++;
+  p.W = windows(p.c);
   p.wbits = 0;
   while ((1 << p.wbits) < p.W) p.wbits++;
   p.end_bit = p.wbits + (p.c - 1) + 1;
   p.sentinel = 1u << (p.wbits + p.c - 1);
   p.nb = (size_t)p.W << (p.c - 1);
   return p;
+}
+
+// *bits = max over i of bitlen(canonical scalar_i)
+__global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scalars, size_t n,
+                                                     unsigned *__restrict__ bits) {
+  unsigned b = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    Fr k = from_mont(scalars[i]);
+    for (int l = 7; l >= 0; l--)
+      if (k.v[l]) {
+        unsigned bl = 32 * l + 32 - __builtin_clz(k.v[l]);
+        b = bl > b ? bl : b;
+        break;
+      }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned x = __shfl_xor(b, o);
+    b = x > b ? x : b;
+  }
+  if ((threadIdx.x & 63) == 0 && b) atomicMax(bits, b);
 }
 
 __global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, size_t n, int c, int W,
@@ -155,9 +176,39 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
   }
 }
 
+// Heavy buckets (skewed scalars: repeated values, small ranges) span many chunks; their
+// chunk heads are summed through a 32-ary hierarchy so no thread walks a long run.
+// Level l >= 1, group g covers chunks [g 32^l, (g+1) 32^l); its sum is formed only when
+// every sorted entry of those chunks has one key (then every head in it is a full-chunk
+// sum of that bucket); other groups are never read by the fixup below.
+constexpr int FIX_FAN = 32;
+constexpr int FIX_LEVELS = 5;
+struct FixLevels {
+  G1Xyzz *lv[FIX_LEVELS + 1];  // lv[l] for l >= 1 (lv[0] unused: the heads live in ht)
+  size_t len[FIX_LEVELS + 1];
+  int n;                        // levels built (0: none)
+};
+
+__global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ keys,
+                                                   const uint32_t *__restrict__ valid_p,
+                                                   const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
+                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out) {
+  const size_t valid = *valid_p;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < n_groups; g += (size_t)gridDim.x * blockDim.x) {
+    size_t span = (size_t)ACC_K;
+    for (int l = 0; l < level; l++) span *= FIX_FAN;
+    const size_t a = g * span, b = a + span;  // entries covered
+    if (b > valid || keys[a] != keys[b - 1]) continue;
+    G1Xyzz acc = level == 1 ? ht[g * FIX_FAN].head : below[g * FIX_FAN];
+    for (int i = 1; i < FIX_FAN; i++)
+      acc = xyzz_add(acc, level == 1 ? ht[g * FIX_FAN + i].head : below[g * FIX_FAN + i]);
+    out[g] = acc;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
                                                       const uint32_t *__restrict__ end,
-                                                      const HeadTail *__restrict__ ht,
+                                                      const HeadTail *__restrict__ ht, FixLevels F,
                                                       G1Xyzz *__restrict__ buckets, size_t nb) {
   for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb;
        bk += (size_t)gridDim.x * blockDim.x) {
@@ -168,8 +219,23 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
     }
     size_t tf = s / ACC_K, tl = (e - 1) / ACC_K;
     if (tf == tl) continue;
-    G1Xyzz acc = ht[tf].tail;
-    for (size_t t = tf + 1; t <= tl; t++) acc = xyzz_add(acc, ht[t].head);
+    G1Xyzz acc = xyzz_add(ht[tf].tail, ht[tl].head);
+    // heads of the chunks strictly inside (tf, tl) -- single-key chunks: peel to
+    // FIX_FAN-aligned ranges, then climb a level
+    size_t lo = tf + 1, hi = tl;
+    int l = 0;
+    for (;;) {
+      auto at = [&](size_t i) { return l == 0 ? ht[i].head : F.lv[l][i]; };
+      if (l == F.n || hi - lo < 2 * FIX_FAN) {
+        for (size_t i = lo; i < hi; i++) acc = xyzz_add(acc, at(i));
+        break;
+      }
+      while (lo % FIX_FAN) acc = xyzz_add(acc, at(lo++));
+      while (hi % FIX_FAN) acc = xyzz_add(acc, at(--hi));
+      lo /= FIX_FAN;
+      hi /= FIX_FAN;
+      l++;
+    }
     buckets[bk] = acc;
   }
 }
@@ -256,7 +322,17 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
     return h;
   }
   if (n >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM larger than 2^31 points");
-  const MsmPlan P = make_plan(n);
+  unsigned bits = 0;
+  {
+    unsigned *d_bits = (unsigned *)ctx->msm_ws[4].ensure(sizeof(unsigned));
+    TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), st));
+    k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, st>>>(scalars, n, d_bits);
+    TNS_LAUNCH_CHECK();
+    TNS_HIP(hipMemcpyAsync(&bits, d_bits, sizeof bits, hipMemcpyDeviceToHost, st));
+    TNS_HIP(hipStreamSynchronize(st));
+  }
+  if (bits == 0) return G1Xyzz::inf();  // all scalars zero
+  const MsmPlan P = make_plan(n, (int)bits);
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
   const int half = 1 << (P.c - 1);
@@ -300,8 +376,31 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
                                                                    points, buckets, ht, nchunks);
     TNS_LAUNCH_CHECK();
   }
-  k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, buckets, P.nb);
-  TNS_LAUNCH_CHECK();
+  {
+    FixLevels F{};
+    size_t groups = nchunks / FIX_FAN;
+    size_t off = 0;
+    while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/32, /1024, ...
+      F.len[F.n + 1] = groups;
+      off += groups;
+      groups /= FIX_FAN;
+      F.n++;
+    }
+    TNS_PROF(ctx, "msm_fixup", 0.0);
+    if (F.n) {
+      G1Xyzz *base = (G1Xyzz *)ctx->fix_ws.ensure(sizeof(G1Xyzz) * off);
+      size_t o = 0;
+      for (int l = 1; l <= F.n; l++) {
+        F.lv[l] = base + o;
+        o += F.len[l];
+        k_fix_level<<<grid_for(F.len[l], 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l, F.len[l],
+                                                                        F.lv[l]);
+        TNS_LAUNCH_CHECK();
+      }
+    }
+    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb);
+    TNS_LAUNCH_CHECK();
+  }
   {
     TNS_PROF(ctx, "msm_reduce", 128.0 * P.nb);
     k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, red_l,

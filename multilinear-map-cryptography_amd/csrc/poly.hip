@@ -11,6 +11,7 @@
 // pass replays each chunk with its carry.  HBM traffic: read c twice, write s once.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "common.hpp"
@@ -213,8 +214,7 @@ static std::vector<G1Affine> build_fixed_base_table() {
   return out;
 }
 
-void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out) {
-  if (!n) return;
+static const G1Affine *upload_fixed_base_table(Ctx *c) {
   static std::vector<G1Affine> host_table;  // constant data; built once per process
   static std::mutex mu;
   {
@@ -224,23 +224,42 @@ void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out) {
   G1Affine *d_table = (G1Affine *)c->scratch[0].ensure(sizeof(G1Affine) * host_table.size());
   TNS_HIP(hipMemcpyAsync(d_table, host_table.data(), sizeof(G1Affine) * host_table.size(),
                          hipMemcpyHostToDevice, c->stream));
-  // process in slabs to bound the XYZZ scratch
+  return d_table;
+}
+
+// out[i] = G * s_i (affine) for canonical scalars, in slabs bounding the XYZZ scratch.
+// fill(off, m, dst) writes the canonical scalars of [off, off + m) into dst (device).
+template <class Fill>
+static void fixed_base_slabs(Ctx *c, size_t n, G1Affine *out, Fill fill) {
+  if (!n) return;
+  const G1Affine *d_table = upload_fixed_base_table(c);
   const size_t slab = (size_t)1 << 22;
   Fr *pw = (Fr *)c->scratch[1].ensure(sizeof(Fr) * std::min(n, slab));
   G1Xyzz *xy = (G1Xyzz *)c->scratch[2].ensure(sizeof(G1Xyzz) * std::min(n, slab));
   Fq *pre = (Fq *)c->scratch[3].ensure(sizeof(Fq) * std::min(n, slab));
   for (size_t off = 0; off < n; off += slab) {
     size_t m = std::min(slab, n - off);
-    size_t chunks = (m + SRS_POW_CHUNK - 1) / SRS_POW_CHUNK;
-    k_tau_powers<<<grid_for(chunks, 256, 1u << 30), 256, 0, c->stream>>>(tau, off, m, pw);
-    TNS_LAUNCH_CHECK();
-    k_fixed_base_mul<<<grid_for(m, 256), 256, 0, c->stream>>>(pw, m, d_table, xy);
+    const Fr *sc = fill(off, m, pw);
+    k_fixed_base_mul<<<grid_for(m, 256), 256, 0, c->stream>>>(sc, m, d_table, xy);
     TNS_LAUNCH_CHECK();
     size_t bchunks = (m + BATCH_INV_CHUNK - 1) / BATCH_INV_CHUNK;
     k_batch_to_affine<<<grid_for(bchunks, 256, 1u << 30), 256, 0, c->stream>>>(xy, m, pre, out + off);
     TNS_LAUNCH_CHECK();
   }
   TNS_HIP(hipStreamSynchronize(c->stream));
+}
+
+void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out) {
+  fixed_base_slabs(c, n, out, [&](size_t off, size_t m, Fr *pw) -> const Fr * {
+    size_t chunks = (m + SRS_POW_CHUNK - 1) / SRS_POW_CHUNK;
+    k_tau_powers<<<grid_for(chunks, 256, 1u << 30), 256, 0, c->stream>>>(tau, off, m, pw);
+    TNS_LAUNCH_CHECK();
+    return pw;
+  });
+}
+
+void fixed_base_mul_dev(Ctx *c, const Fr *scalars_canon, size_t n, G1Affine *out) {
+  fixed_base_slabs(c, n, out, [&](size_t off, size_t, Fr *) -> const Fr * { return scalars_canon + off; });
 }
 
 }  // namespace tns

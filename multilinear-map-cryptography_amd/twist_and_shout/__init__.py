@@ -141,6 +141,11 @@ class Context:
                 cls._by_device[device] = Context(device)
             return cls._by_device[device]
 
+    def set_commit_basis(self, lagrange: bool):
+        """True (default): Twist/Shout commit and open through the SRS's Lagrange basis
+        when it has tau; False: vector_to_polynomial + coefficient KZG.  Same proofs."""
+        _check(N.load().tns_ctx_set_commit_basis(self.handle, 1 if lagrange else 0))
+
     def timing(self):
         out = (C.c_double * 6)()
         N.load().tns_last_prove_timing(self.handle, out)
@@ -161,6 +166,15 @@ class Srs:
 
     def __len__(self):
         return N.load().tns_srs_len(self.handle)
+
+    def set_tau(self, tau: int):
+        """Attach the setup trapdoor (CommitmentParams.tau) so the Lagrange basis exists."""
+        _check(N.load().tns_srs_set_tau(self.handle, N.p64(to_mont([tau]))))
+
+    def prepare_lagrange(self, n: int):
+        """Build the Lagrange basis for n = 2^k nodes now (setup time) instead of at the
+        first proof of that size."""
+        _check(N.load().tns_srs_prepare_lagrange(self.ctx.handle, self.handle, n))
 
     def download(self, n: Optional[int] = None) -> np.ndarray:
         n = len(self) if n is None else n
@@ -203,7 +217,10 @@ class CommitmentParams:
                     arr[i] = 0
         h = C.c_void_p()
         _check(N.load().tns_srs_upload(ctx.handle, N.p64(arr), len(arr), C.byref(h)))
-        return cls(Srs(ctx, h), tau)
+        srs = Srs(ctx, h)
+        if tau is not None:
+            srs.set_tau(tau)
+        return cls(srs, tau)
 
 
 @dataclass
@@ -340,6 +357,27 @@ class KZGCommitment:
         pi = np.zeros(12, dtype=np.uint64)
         _check(N.load().tns_kzg_open(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(c)), len(c),
                                      N.p64(z), N.p64(v), N.p64(pi)))
+        return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
+
+
+    @staticmethod
+    def commit_evaluations(params: CommitmentParams, evaluations) -> KZGCommitmentValue:
+        """commit(vector_to_polynomial(evaluations)) as Twist/Shout::prove do (len a power of two)."""
+        y = _as_mont(evaluations)
+        out = np.zeros(12, dtype=np.uint64)
+        _check(N.load().tns_kzg_commit_evals(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(y)),
+                                             len(y), N.p64(out)))
+        return KZGCommitmentValue(_g1_from_proj(out), out)
+
+    @staticmethod
+    def open_evaluations(params: CommitmentParams, evaluations, point: int) -> Tuple[int, KZGProof]:
+        """open(vector_to_polynomial(evaluations), point) as Twist/Shout::prove do."""
+        y = _as_mont(evaluations)
+        z = to_mont([point])[0]
+        v = np.zeros(4, dtype=np.uint64)
+        pi = np.zeros(12, dtype=np.uint64)
+        _check(N.load().tns_kzg_open_evals(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(y)), len(y),
+                                           N.p64(z), N.p64(v), N.p64(pi)))
         return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
 
 
@@ -702,7 +740,7 @@ def profile_enable(ctx: Context, on: bool = True):
     N.load().tns_profile_enable(ctx.handle, 1 if on else 0)
 
 
-PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_reduce", "ntt_stage", "ntt_lds",
+PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_fixup", "msm_reduce", "ntt_stage", "ntt_lds",
                   "ntt_pointwise", "interp_tile", "interp_elementwise", "sumcheck_round", "open_scan"]
 
 

@@ -75,8 +75,13 @@ SIGNATURES = [
     ("tns_srs_download", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t]),
     ("tns_srs_len", C.c_size_t, [C.c_void_p]),
     ("tns_srs_destroy", None, [C.c_void_p]),
+    ("tns_srs_set_tau", C.c_int, [C.c_void_p, U64P]),
+    ("tns_srs_prepare_lagrange", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("tns_ctx_set_commit_basis", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_kzg_commit", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_kzg_open", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
+    ("tns_kzg_commit_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
+    ("tns_kzg_open_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
     ("tns_commitment_hash", C.c_int, [U64P, U64P]),
     ("tns_msm", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_interpolate_consecutive", C.c_int, [C.c_void_p, U64P, C.c_size_t, U64P]),

@@ -116,6 +116,35 @@ def test_msm_large_trapdoor(L):
     assert got == po.affine_mul(po.G1_GEN, s)
 
 
+@pytest.mark.parametrize("pattern", ["equal", "tiny", "addr22", "flags", "half_equal", "pow2"])
+def test_msm_skewed_scalars_large(pattern):
+    """Heavy buckets (one bucket holding up to all 2^20 entries) and narrow scalars (the
+    bit-length-adaptive window plan) -- the shapes Twist commits produce."""
+    pp, _ = params(18)
+    n = 1 << 20
+    rng = np.random.default_rng(hash(pattern) % 2**32)
+    if pattern == "equal":
+        vals = [2**200 + 12345] * n
+    elif pattern == "tiny":
+        vals = [int(x) for x in rng.integers(0, 3, size=n)]
+    elif pattern == "addr22":
+        vals = [int(x) for x in rng.integers(0, 1 << 22, size=n)]
+    elif pattern == "flags":
+        vals = [int(x) for x in rng.integers(0, 2, size=n)]
+    elif pattern == "half_equal":
+        r = rand_fr_mont(n // 2, seed=5)
+        vals = [R - 7] * (n // 2) + ts.from_mont(r)
+    else:  # powers of two: one nonzero digit per scalar, spread over every window
+        vals = [1 << int(x) for x in rng.integers(0, 254, size=n)]
+    c = ts.to_mont(vals)
+    got = ts.msm(pp.commitment_params, c)
+    tau = pp.commitment_params.tau
+    s = 0
+    for v in reversed(vals):
+        s = (s * tau + v) % R
+    assert got == po.affine_mul(po.G1_GEN, s)
+
+
 def test_commit_beyond_srs_is_commitment_error():
     pp, _ = params(1)  # 9 SRS points
     with pytest.raises(ts.CommitmentError):
