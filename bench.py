@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--commit-basis", choices=["lagrange", "coefficients"], default="lagrange",
                     help="prove via the setup's Lagrange-basis SRS (default) or via interpolation + "
                          "coefficient KZG (the reference's route); identical proofs")
+    ap.add_argument("--no-msm-tables", action="store_true",
+                    help="per-window MSM buckets instead of the fixed-base window tables")
     return ap.parse_args()
 
 
@@ -144,6 +146,7 @@ def main():
     n_ops = 1 << log_ops
     L = log_ops - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
     ctx.set_commit_basis(args.commit_basis == "lagrange")
+    ctx.set_msm_tables(not args.no_msm_tables)
     t_setup = time.perf_counter()
     pp, _ = ts.setup_params(L, device=local)
     t_setup = time.perf_counter() - t_setup

@@ -122,6 +122,10 @@ int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n);
  * basis when the SRS has tau; 0 forces vector_to_polynomial + coefficient KZG
  * (src/twist.rs:151-163).  Both produce identical proofs. */
 int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange);
+/* MSM over a fixed base (SRS, Lagrange basis): on != 0 (default) uses the base's
+ * window-shifted table (built once, W copies of the points) so that every window shares
+ * one bucket set; 0 forces the per-window bucket layout.  Same results. */
+int tns_ctx_set_msm_tables(tns_ctx *ctx, int on);
 
 /* ---------------------------------------------------------------- KZG (src/commitments.rs) */
 /* CommitmentScheme::commit for KZGCommitment (src/commitments.rs:162-180).

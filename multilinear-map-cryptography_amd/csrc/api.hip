@@ -84,7 +84,7 @@ struct Timer {
 // KZGCommitment::commit on device-resident coefficients (src/commitments.rs:162-180)
 static G1Affine commit_dev(Ctx *c, const Srs &srs, const Fr *coeffs, size_t n) {
   if (n > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
-  return xyzz_to_affine(msm_dev(c, srs.points.as<G1Affine>(), coeffs, n));
+  return xyzz_to_affine(msm_dev(c, srs.points.as<G1Affine>(), coeffs, n, srs_fixed_base(c, srs, n)));
 }
 
 // KZGCommitment::open on device-resident coefficients (src/commitments.rs:182-199)
@@ -109,14 +109,14 @@ struct EvalPoly {
   const Fr *y = nullptr;       // device, N (must stay intact until opened)
   Fr *coeffs = nullptr;        // device scratch, N (coefficient path)
   size_t N = 0;
-  const G1Affine *basis = nullptr;
+  const LagrangeBasis *basis = nullptr;
   bool have_coeffs = false;
 };
 
 static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p) {
   if (p.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
   p.basis = lagrange_basis_dev(c, srs, p.N);
-  if (p.basis) return xyzz_to_affine(msm_dev(c, p.basis, p.y, p.N));
+  if (p.basis) return xyzz_to_affine(msm_dev(c, p.basis->points.as<G1Affine>(), p.y, p.N, p.basis->fb));
   interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
   p.have_coeffs = true;
   return commit_dev(c, srs, p.coeffs, p.N);
@@ -127,7 +127,7 @@ static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *val
   if (p.basis) {
     Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.N);
     if (lagrange_quotient_dev(c, p.y, p.N, z, value, q)) {
-      *proof = xyzz_to_affine(msm_dev(c, p.basis, q, p.N));
+      *proof = xyzz_to_affine(msm_dev(c, p.basis->points.as<G1Affine>(), q, p.N, p.basis->fb));
       return;
     }
   }
@@ -286,9 +286,17 @@ int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n) {
     if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
     const bool saved = ctx->c.lagrange_commit;
     ctx->c.lagrange_commit = true;
-    const G1Affine *b = lagrange_basis_dev(&ctx->c, srs->s, n);
+    const LagrangeBasis *b = lagrange_basis_dev(&ctx->c, srs->s, n);
     ctx->c.lagrange_commit = saved;
     (void)b;  // nullptr only when tau is itself a node: the coefficient path is used then
+    return TNS_OK;
+  });
+}
+
+int tns_ctx_set_msm_tables(tns_ctx *ctx, int on) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.msm_tables = on != 0;
     return TNS_OK;
   });
 }

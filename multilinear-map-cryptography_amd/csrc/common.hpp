@@ -78,6 +78,20 @@ struct InterpPlan {
   std::vector<size_t> level_off;    // element offset of level l (m = 2^l) in level_tables
 };
 
+// Window-shifted copies of a fixed point set for the shared-bucket MSM (msm.hip):
+// table[j n + i] = 2^(c j) P_i, j < W.
+struct FixedBase {
+  DevBuf table;
+  size_t n = 0;
+  int c = 0, W = 0;
+};
+
+struct LagrangeBasis {
+  DevBuf points;             // G1Affine[N]: G * L_j(tau)
+  FixedBase *fb = nullptr;   // its window table (N >= 2^12)
+  ~LagrangeBasis() { delete fb; }
+};
+
 struct Srs {
   DevBuf points;  // G1Affine[n]
   size_t n = 0;
@@ -86,12 +100,14 @@ struct Srs {
   // also yields the Lagrange basis of the nodes {0..N-1}: G * L_j(tau) (lagrange.hip).
   bool has_tau = false;
   Fr tau;
-  mutable std::map<unsigned, DevBuf *> lagrange;  // log N -> G1Affine[N] (cache)
+  mutable std::map<unsigned, LagrangeBasis *> lagrange;  // log N -> basis (cache)
+  mutable FixedBase *fb = nullptr;                        // window table of `points` (lazy)
   Srs() = default;
   Srs(const Srs &) = delete;
   Srs &operator=(const Srs &) = delete;
   ~Srs() {
     for (auto &kv : lagrange) delete kv.second;
+    delete fb;
   }
 };
 
@@ -166,6 +182,7 @@ struct Ctx {
   std::map<uint32_t, DevBuf *> pass_tw;  // four-step pass twiddles keyed by (lo << 8 | r)
   std::map<unsigned, DevBuf *> bary_w;   // log N -> barycentric weights of nodes {0..N-1}
   bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
+  bool msm_tables = true;                // shared-bucket MSM on fixed bases with window tables
   KernelProfiler prof;
   ~Ctx();
 };
@@ -224,8 +241,11 @@ void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out);
 void to_mont_u64_dev(Ctx *c, const uint64_t *in, Fr *out, size_t n);
 void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 
-// msm.hip
-G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n);
+// msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
+G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr);
+FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
+// the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
+const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);
 
 // interp.hip
 void interpolate_consecutive_dev(Ctx *c, const Fr *y, size_t n, Fr *coeffs);
@@ -233,11 +253,12 @@ void factorial_tables_dev(Ctx *c, size_t nf, Fr *fact, Fr *ifact);
 
 // poly.hip: out[i] = G * s_i (affine), scalars canonical
 void fixed_base_mul_dev(Ctx *c, const Fr *scalars_canon, size_t n, G1Affine *out);
+void xyzz_to_affine_batch_dev(Ctx *c, const G1Xyzz *in, size_t n, G1Affine *out, Fq *prefix_scratch);
 
 // lagrange.hip: KZG on evaluations over the nodes {0..N-1}
 // Lagrange basis G * L_j(tau) for N (cached in srs); nullptr when srs has no tau or
 // tau is itself a node.
-const G1Affine *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N);
+const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N);
 // v = P(z) and q(j) = (P(j) - v) / (j - z) on the nodes (q: device, N), for z not a
 // node; returns false (nothing written) when z is a node.
 bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q);

@@ -174,12 +174,12 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &x, size_t N, Fr *pre) {
   return s;
 }
 
-const G1Affine *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N) {
+const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N) {
   if (!c->lagrange_commit || !srs.has_tau || N == 0 || (N & (N - 1))) return nullptr;
   if (is_node(srs.tau, N)) return nullptr;
   const unsigned lg = ilog2_exact(N);
   auto it = srs.lagrange.find(lg);
-  if (it != srs.lagrange.end()) return it->second->as<G1Affine>();
+  if (it != srs.lagrange.end()) return it->second;
   const Fr *w = bary_weights(c, N);
   DevBuf scal;
   Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * N);  // pre, then canonical L_j(tau) in place
@@ -187,16 +187,17 @@ const G1Affine *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N) {
   k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(srs.tau, N, s.T, s.Tm, sc, s.cp, w,
                                                                            nullptr, s.dev, sc, nullptr);
   TNS_LAUNCH_CHECK();
-  DevBuf *b = new DevBuf();
+  LagrangeBasis *b = new LagrangeBasis();
   try {
-    G1Affine *pts = (G1Affine *)b->ensure(sizeof(G1Affine) * N);
+    G1Affine *pts = (G1Affine *)b->points.ensure(sizeof(G1Affine) * N);
     fixed_base_mul_dev(c, sc, N, pts);  // synchronises
+    if (N >= ((size_t)1 << 12)) b->fb = fixed_base_build_dev(c, pts, N);
   } catch (...) {
     delete b;
     throw;
   }
   srs.lagrange[lg] = b;
-  return b->as<G1Affine>();
+  return b;
 }
 
 bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q) {

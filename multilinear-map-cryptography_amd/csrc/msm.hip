@@ -4,66 +4,97 @@
 // (src/commitments.rs:173-177): C = sum_i c_i * g1_powers[i].  The group element
 // is unique, so any correct algorithm reproduces it exactly.
 //
+// Two bucket layouts share one pipeline:
+//  * per-window: W windows of c bits, W * 2^(c-1) buckets, windows combined by Horner;
+//  * shared (fixed bases: the SRS and its Lagrange bases never change): a precomputed
+//    table T[j n + i] = 2^(c j) P_i turns window j's digit of scalar i into a digit of
+//    point T[j n + i], so all windows land in ONE set of 2^(c-1) buckets -- the bucket
+//    reduction runs once instead of W times, no Horner doublings remain, and a wider c
+//    (fewer windows, fewer bucket additions) becomes affordable.
+//
 // Pipeline (all on one stream):
-//  1. k_digits: scalar -> canonical -> W signed c-bit digits; key = (window, |d|-1),
-//     value = point index | sign<<31; zero digits get a sentinel key.
-//  2. rocPRIM/hipCUB radix sort of the W*n (key, value) pairs by key.
+//  0. k_scalar_bits: bit length of the largest scalar -> windows above it are skipped
+//     (trace commitments -- addresses, small values, flags -- are narrow).
+//  1. k_digits: scalar -> canonical -> W signed c-bit digits; key = bucket, value =
+//     point index | sign<<31; zero digits get a sentinel key.
+//  2. rocPRIM/hipCUB radix sort of the (key, value) pairs by key.
 //  3. k_bucket_bounds: [start, end) of every bucket in the sorted order.
-//  4. k_accumulate: load-balanced -- each thread owns K consecutive sorted entries
-//     and XYZZ-madds the (possibly negated) affine points run by run; runs that
-//     cross a chunk boundary leave a head/tail partial.
-//  5. k_bucket_fixup: buckets spanning chunks = tail + heads; empty -> identity.
-//  6. k_bucket_reduce + k_window_sum: S_w = sum_j (j+1) B_{w,j} via per-group
-//     running sums, then a block tree per window.
-//  7. host: sum_w 2^(c w) S_w (Horner, W*c doublings).
+//  4. k_accumulate: load-balanced -- each thread owns ACC_K consecutive sorted entries
+//     and XYZZ-madds the (possibly negated) affine points run by run; runs that cross a
+//     chunk boundary leave a head/tail partial; k_bucket_fixup completes those buckets (heavy buckets'
+//     chunk heads through FIX_FAN-ary level sums, so no thread walks a long run).
+//  5. k_reduce_level: per group of L buckets of a window, running sums
+//     T_g = sum_{j in g} (j - a + 1) B_j and S_g = sum_{j in g} B_j; then
+//     sum_j (j+1) B_j = sum_g T_g + L sum_g g S_g, and sum_g g S_g = sum_b 2^b M_b with
+//     M_b the sum of the S_g whose index has bit b set: k_masked_sums + chunked sums
+//     (short dependency chains -- single-thread point-add chains are the slow part).
+//  6. host: per-window Horner (per-window layout) or nothing (shared layout).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <vector>
 
 #include "common.hpp"
 
 namespace tns {
 
-constexpr int ACC_K = 32;      // sorted entries per accumulation thread
-constexpr int RED_L = 16;      // buckets per reduction thread
+constexpr int ACC_K = 32;  // sorted entries per accumulation thread
+constexpr int RED_L = 16;  // running-sum group size of the bucket reduction
 
 struct MsmPlan {
-  int c, W, wbits;
-  uint32_t sentinel;
-  int end_bit;
-  size_t nb;  // W * 2^(c-1)
+  bool shared = false;  // fixed-base shared-bucket layout
+  int c = 0, W = 0, wbits = 0;
+  uint32_t sentinel = 0;
+  int end_bit = 0;
+  size_t nb = 0;      // buckets in total
+  int Wr = 0;         // bucket sets (windows) to reduce: W (per-window) or 1 (shared)
+  size_t half = 0;    // buckets per set, 2^(c-1)
+  size_t stride = 0;  // shared: table stride n_table (value = j * stride + i)
 };
 
-// bits: bit length of the largest scalar (the windows above it are all zero; commitments
-// to traces -- addresses, small values, flags -- often have bits << 254)
-static MsmPlan make_plan(size_t n, int bits) {
-  MsmPlan p;
+// signed-digit windows of c bits for `bits`-bit scalars: the top window's raw value
+// < 2^(bits - c(W-1)) must stay <= 2^(c-1) so that it never carries out
+static int windows_for(int bits, int c) {
+  int W = (bits + c - 1) / c;
+  if (bits - c * (W - 1) > c - 1) W++;
+  return W;
+}
+
+// bucket additions + ~3 additions per bucket in the reduction
+static double plan_cost(size_t n, int W, int c, int sets) {
+  return (double)W * (double)n + 3.0 * sets * (double)((size_t)1 << (c - 1));
+}
+
+static int best_window(size_t n, int bits, int cmax, bool shared) {
   int lg = 0;
   while (((size_t)1 << lg) < n) lg++;
-  // the top window must not produce a carry: its raw value < 2^(bits - c(W-1)) must be <= 2^(c-1)
-  auto windows = [bits](int c) {
-    int W = (bits + c - 1) / c;
-    if (bits - c * (W - 1) > c - 1) W++;
-    return W;
-  };
-  // window c minimising (bucket adds) W*n + (reduction adds) ~3*W*2^(c-1)
   double best = 1e300;
-  p.c = 4;
-  for (int c = 4; c <= 20 && c <= lg + 1; c++) {
-    double cost = (double)windows(c) * (double)n + 3.0 * windows(c) * (double)(1u << (c - 1));
+  int bc = 4;
+  for (int c = 4; c <= cmax && c <= lg + 2; c++) {
+    const int W = windows_for(bits, c);
+    const double cost = plan_cost(n, W, c, shared ? 1 : W);
     if (cost < best * 0.98) {  // prefer the smaller window on near-ties (less bucket memory)
       best = cost;
-      p.c = c;
+      bc = c;
     }
   }
-  p.W = windows(p.c);
-  p.wbits = 0;
-  while ((1 << p.wbits) < p.W) p.wbits++;
+  return bc;
+}
+
+static void finish_plan(MsmPlan &p) {
+  p.half = (size_t)1 << (p.c - 1);
+  if (p.shared) {
+    p.wbits = 0;
+    p.Wr = 1;
+  } else {
+    p.wbits = 0;
+    while ((1 << p.wbits) < p.W) p.wbits++;
+    p.Wr = p.W;
+  }
   p.end_bit = p.wbits + (p.c - 1) + 1;
   p.sentinel = 1u << (p.wbits + p.c - 1);
-  p.nb = (size_t)p.W << (p.c - 1);
-  return p;
+  p.nb = (size_t)p.Wr * p.half;
 }
 
 // *bits = max over i of bitlen(canonical scalar_i)
@@ -86,9 +117,11 @@ __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scal
   if ((threadIdx.x & 63) == 0 && b) atomicMax(bits, b);
 }
 
+// shared = false: key = (w << (c-1)) | (|d| - 1), value = i | sign<<31
+// shared = true:  key = |d| - 1,                  value = (w * stride + i) | sign<<31
 __global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, size_t n, int c, int W,
-                                                uint32_t sentinel, uint32_t *__restrict__ keys,
-                                                uint32_t *__restrict__ vals) {
+                                                uint32_t sentinel, bool shared, uint32_t stride,
+                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
     Fr k = from_mont(scalars[i]);
@@ -101,7 +134,7 @@ __global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, 
       uint64_t hi = limb + 1 < 8 ? k.v[limb + 1] : 0;
       uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1u << c) - 1));
       uint32_t val = raw + carry;
-      uint32_t key, neg = 0, mag;
+      uint32_t neg = 0, mag;
       if (val > half) {
         mag = (1u << c) - val;
         neg = 1;
@@ -110,9 +143,9 @@ __global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, 
         mag = val;
         carry = 0;
       }
-      key = mag ? (((uint32_t)w << (c - 1)) | (mag - 1)) : sentinel;
+      uint32_t key = mag ? ((shared ? 0u : ((uint32_t)w << (c - 1))) | (mag - 1)) : sentinel;
       keys[(size_t)w * n + i] = key;
-      vals[(size_t)w * n + i] = (uint32_t)i | (neg << 31);
+      vals[(size_t)w * n + i] = (uint32_t)(shared ? (size_t)w * stride + i : i) | (neg << 31);
     }
   }
 }
@@ -155,15 +188,13 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
        t += (size_t)gridDim.x * blockDim.x) {
     const size_t a = t * ACC_K;
     if (a >= valid) continue;
-    size_t b = a + ACC_K;
-    if (b > valid) b = valid;
+    const size_t b = a + ACC_K < valid ? a + ACC_K : valid;
     uint32_t cur = keys[a];
     G1Xyzz acc = G1Xyzz::inf();
     for (size_t p = a;; p++) {
-      uint32_t k = (p < b) ? keys[p] : 0xffffffffu;
-      if (k != cur) {
-        // flush run of bucket `cur`
-        uint32_t s = start[cur], e = end[cur];
+      const uint32_t k = (p < b) ? keys[p] : 0xffffffffu;
+      if (k != cur) {  // flush the run of bucket `cur`
+        const uint32_t s = start[cur], e = end[cur];
         if (s < a) ht[t].head = acc;
         else if (e > b) ht[t].tail = acc;
         else buckets[cur] = acc;
@@ -177,14 +208,14 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
 }
 
 // Heavy buckets (skewed scalars: repeated values, small ranges) span many chunks; their
-// chunk heads are summed through a 32-ary hierarchy so no thread walks a long run.
-// Level l >= 1, group g covers chunks [g 32^l, (g+1) 32^l); its sum is formed only when
+// chunk heads are summed through a FIX_FAN-ary hierarchy so no thread walks a long run.
+// Level l >= 1, group g covers chunks [g F^l, (g+1) F^l) (F = FIX_FAN); its sum is formed only when
 // every sorted entry of those chunks has one key (then every head in it is a full-chunk
-// sum of that bucket); other groups are never read by the fixup below.
-constexpr int FIX_FAN = 32;
-constexpr int FIX_LEVELS = 5;
+// sum of that bucket); other groups are never read.
+constexpr int FIX_FAN = 8;  // short peel chains: single-thread add chains are latency-bound
+constexpr int FIX_LEVELS = 8;
 struct FixLevels {
-  G1Xyzz *lv[FIX_LEVELS + 1];  // lv[l] for l >= 1 (lv[0] unused: the heads live in ht)
+  G1Xyzz *lv[FIX_LEVELS + 1];  // lv[l] for l >= 1 (the level-0 heads live in ht)
   size_t len[FIX_LEVELS + 1];
   int n;                        // levels built (0: none)
 };
@@ -206,63 +237,93 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
   }
 }
 
+// bucket values: empty -> identity; a run inside one chunk is already in buckets[bk];
+// a run across chunks tf < tl -> tail(tf) + heads of (tf, tl) (via the levels) + head(tl)
 __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
                                                       const uint32_t *__restrict__ end,
                                                       const HeadTail *__restrict__ ht, FixLevels F,
                                                       G1Xyzz *__restrict__ buckets, size_t nb) {
   for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb;
        bk += (size_t)gridDim.x * blockDim.x) {
-    uint32_t s = start[bk], e = end[bk];
+    const uint32_t s = start[bk], e = end[bk];
     if (s == e) {
       buckets[bk] = G1Xyzz::inf();
       continue;
     }
-    size_t tf = s / ACC_K, tl = (e - 1) / ACC_K;
+    const size_t tf = s / ACC_K, tl = (e - 1) / ACC_K;
     if (tf == tl) continue;
-    G1Xyzz acc = xyzz_add(ht[tf].tail, ht[tl].head);
-    // heads of the chunks strictly inside (tf, tl) -- single-key chunks: peel to
-    // FIX_FAN-aligned ranges, then climb a level
+    // one addition site: the items are head(tl), then the inner heads (tf, tl), peeled
+    // to FIX_FAN-aligned ranges and climbing a level whenever both ends are aligned
+    G1Xyzz acc = ht[tf].tail;
     size_t lo = tf + 1, hi = tl;
     int l = 0;
+    bool pending_head = true;
     for (;;) {
-      auto at = [&](size_t i) { return l == 0 ? ht[i].head : F.lv[l][i]; };
-      if (l == F.n || hi - lo < 2 * FIX_FAN) {
-        for (size_t i = lo; i < hi; i++) acc = xyzz_add(acc, at(i));
-        break;
+      const G1Xyzz *item;
+      if (pending_head) {
+        item = &ht[tl].head;
+        pending_head = false;
+      } else {
+        if (lo >= hi) break;
+        const bool climb = l < F.n && hi - lo >= 2 * FIX_FAN;
+        if (climb && lo % FIX_FAN == 0 && hi % FIX_FAN == 0) {
+          lo /= FIX_FAN;
+          hi /= FIX_FAN;
+          l++;
+          continue;
+        }
+        size_t i;
+        if (!climb || lo % FIX_FAN) i = lo++;
+        else i = --hi;  // lo aligned, hi not
+        item = l == 0 ? &ht[i].head : &F.lv[l][i];
       }
-      while (lo % FIX_FAN) acc = xyzz_add(acc, at(lo++));
-      while (hi % FIX_FAN) acc = xyzz_add(acc, at(--hi));
-      lo /= FIX_FAN;
-      hi /= FIX_FAN;
-      l++;
+      acc = xyzz_add(acc, *item);
     }
     buckets[bk] = acc;
   }
 }
 
-// per (window, group): sum_{j in group} (j+1) B_j
-__global__ void __launch_bounds__(256) k_bucket_reduce(const G1Xyzz *__restrict__ buckets, int W,
-                                                       int half_buckets, int red_l, G1Xyzz *__restrict__ out) {
-  const int groups = half_buckets / red_l;
-  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)W * groups;
+// one level over X (sets x n): groups of L; T = sum (j - a + 1) X_j, S = sum X_j
+__global__ void __launch_bounds__(64) k_reduce_level(const G1Xyzz *__restrict__ X, int sets, size_t n, int L,
+                                                     G1Xyzz *__restrict__ T, G1Xyzz *__restrict__ S) {
+  const size_t groups = n / L;
+  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)sets * groups;
        id += (size_t)gridDim.x * blockDim.x) {
-    int w = (int)(id / groups), g = (int)(id % groups);
-    const G1Xyzz *B = buckets + (size_t)w * half_buckets;
-    int a = g * red_l;
+    const size_t r = id / groups, g = id % groups;
+    const G1Xyzz *x = X + r * n + g * L;
     G1Xyzz run = G1Xyzz::inf(), acc = G1Xyzz::inf();
-    for (int j = a + red_l - 1; j >= a; j--) {
-      run = xyzz_add(run, B[j]);
+    for (int j = L - 1; j >= 0; j--) {
+      run = xyzz_add(run, x[j]);
       acc = xyzz_add(acc, run);
     }
-    if (a) acc = xyzz_add(acc, xyzz_mul_small(run, (uint64_t)a));
-    out[id] = acc;
+    T[id] = acc;
+    S[id] = run;
   }
 }
 
-// out[t] = sum of in[t*chunk .. (t+1)*chunk): shrinks the per-window partial count in
-// parallel before the one-block-per-window tree (windows stay contiguous: chunk | groups).
-__global__ void __launch_bounds__(256) k_sum_chunks(const G1Xyzz *__restrict__ in, size_t n_out, int chunk,
-                                                    G1Xyzz *__restrict__ out) {
+// parts[(r specs + s) nch + ch] over the groups gi of chunk ch of set r:
+//   s < nbits: sum of S[gi] with bit s of gi set;  s == nbits: sum of T[gi]
+__global__ void __launch_bounds__(64) k_masked_sums(const G1Xyzz *__restrict__ T, const G1Xyzz *__restrict__ S,
+                                                    int sets, size_t g, int nbits, int CH,
+                                                    G1Xyzz *__restrict__ parts) {
+  const int specs = nbits + 1;
+  const size_t nch = g / CH;
+  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)sets * specs * nch;
+       id += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = id / (specs * nch), rem = id % (specs * nch);
+    const int sp = (int)(rem / nch);
+    const size_t ch = rem % nch;
+    const G1Xyzz *src = (sp == nbits ? T : S) + r * g;
+    G1Xyzz acc = G1Xyzz::inf();
+    for (size_t gi = ch * CH; gi < ch * CH + CH; gi++)
+      if (sp == nbits || ((gi >> sp) & 1)) acc = xyzz_add(acc, src[gi]);
+    parts[id] = acc;
+  }
+}
+
+// out[t] = sum of in[t*chunk .. (t+1)*chunk)
+__global__ void __launch_bounds__(64) k_sum_chunks(const G1Xyzz *__restrict__ in, size_t n_out, int chunk,
+                                                   G1Xyzz *__restrict__ out) {
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n_out; t += (size_t)gridDim.x * blockDim.x) {
     G1Xyzz acc = in[t * chunk];
     for (int i = 1; i < chunk; i++) acc = xyzz_add(acc, in[t * chunk + i]);
@@ -270,19 +331,20 @@ __global__ void __launch_bounds__(256) k_sum_chunks(const G1Xyzz *__restrict__ i
   }
 }
 
-__global__ void __launch_bounds__(256) k_window_sum(const G1Xyzz *__restrict__ parts, int groups,
-                                                    G1Xyzz *__restrict__ out) {
+// out[r] = sum of parts[r*groups .. (r+1)*groups), one block per set
+__global__ void __launch_bounds__(256) k_set_sum(const G1Xyzz *__restrict__ parts, size_t groups,
+                                                 G1Xyzz *__restrict__ out) {
   __shared__ G1Xyzz lds[256];
-  const int w = blockIdx.x;
+  const size_t r = blockIdx.x;
   G1Xyzz acc = G1Xyzz::inf();
-  for (int g = threadIdx.x; g < groups; g += blockDim.x) acc = xyzz_add(acc, parts[(size_t)w * groups + g]);
+  for (size_t g = threadIdx.x; g < groups; g += blockDim.x) acc = xyzz_add(acc, parts[r * groups + g]);
   lds[threadIdx.x] = acc;
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
     if ((int)threadIdx.x < s) lds[threadIdx.x] = xyzz_add(lds[threadIdx.x], lds[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[w] = lds[0];
+  if (threadIdx.x == 0) out[r] = lds[0];
 }
 
 // Naive path for tiny inputs: one thread per point, double-and-add, then a tree.
@@ -309,7 +371,77 @@ __global__ void __launch_bounds__(64) k_msm_tiny(const G1Affine *__restrict__ pt
   if (threadIdx.x == 0) *out = lds[0];
 }
 
-G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
+// ---------------------------------------------------------------- fixed-base tables
+__global__ void __launch_bounds__(256) k_affine_to_xyzz(const G1Affine *__restrict__ in, size_t n,
+                                                        G1Xyzz *__restrict__ out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = xyzz_from_affine(in[i]);
+}
+
+__global__ void __launch_bounds__(256) k_dbl_times(G1Xyzz *__restrict__ x, size_t n, int times) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    G1Xyzz p = x[i];
+    for (int k = 0; k < times; k++) p = xyzz_dbl(p);
+    x[i] = p;
+  }
+}
+
+// the window a table for n points uses: the shared-layout optimum for full-width scalars
+static int table_window(size_t n) { return best_window(n, 254, 22, true); }
+
+FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n) {
+  FixedBase *fb = new FixedBase();
+  try {
+    fb->n = n;
+    fb->c = table_window(n);
+    fb->W = windows_for(254, fb->c);
+    G1Affine *T = (G1Affine *)fb->table.ensure(sizeof(G1Affine) * n * fb->W);
+    TNS_HIP(hipMemcpyAsync(T, points, sizeof(G1Affine) * n, hipMemcpyDeviceToDevice, c->stream));
+    const size_t slab = std::min(n, (size_t)1 << 22);
+    DevBuf xb, pb;
+    G1Xyzz *X = (G1Xyzz *)xb.ensure(sizeof(G1Xyzz) * slab);
+    Fq *pre = (Fq *)pb.ensure(sizeof(Fq) * slab);
+    for (size_t off = 0; off < n; off += slab) {
+      const size_t m = std::min(slab, n - off);
+      k_affine_to_xyzz<<<grid_for(m, 256), 256, 0, c->stream>>>(points + off, m, X);
+      TNS_LAUNCH_CHECK();
+      for (int j = 1; j < fb->W; j++) {
+        k_dbl_times<<<grid_for(m, 256), 256, 0, c->stream>>>(X, m, fb->c);
+        TNS_LAUNCH_CHECK();
+        xyzz_to_affine_batch_dev(c, X, m, T + (size_t)j * n + off, pre);
+      }
+    }
+    TNS_HIP(hipStreamSynchronize(c->stream));
+  } catch (...) {
+    delete fb;
+    throw;
+  }
+  return fb;
+}
+
+const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n) {
+  if (n < ((size_t)1 << 16) || !c->msm_tables) return nullptr;
+  if (!srs.fb) srs.fb = fixed_base_build_dev(c, srs.points.as<G1Affine>(), srs.n);
+  return srs.fb;
+}
+
+// ---------------------------------------------------------------- driver
+// sum over each set of the sets x n array X (device) -> out (sets, device)
+static void sum_sets(Ctx *ctx, G1Xyzz *X, int sets, size_t n, G1Xyzz *tmp, G1Xyzz *out) {
+  hipStream_t st = ctx->stream;
+  G1Xyzz *src = X, *dst = tmp;
+  while (n > 128 && n % 8 == 0) {  // short chains: these passes are latency-bound
+    const size_t n_out = (size_t)sets * (n / 8);
+    k_sum_chunks<<<grid_for(n_out, 64, 1u << 30), 64, 0, st>>>(src, n_out, 8, dst);
+    TNS_LAUNCH_CHECK();
+    std::swap(src, dst);
+    n /= 8;
+  }
+  k_set_sum<<<sets, 256, 0, st>>>(src, n, out);
+  TNS_LAUNCH_CHECK();
+}
+
+G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb) {
   if (n == 0) return G1Xyzz::inf();
   hipStream_t st = ctx->stream;
   if (n <= 64) {
@@ -332,10 +464,24 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
     TNS_HIP(hipStreamSynchronize(st));
   }
   if (bits == 0) return G1Xyzz::inf();  // all scalars zero
-  const MsmPlan P = make_plan(n, (int)bits);
+
+  // plan: per-window layout, or the shared layout when a fixed-base table covers the points
+  MsmPlan P;
+  P.c = best_window(n, (int)bits, 20, false);
+  P.W = windows_for((int)bits, P.c);
+  if (fb && ctx->msm_tables && fb->n >= n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
+    const int Ws = windows_for((int)bits, fb->c);
+    if (Ws <= fb->W && plan_cost(n, Ws, fb->c, 1) < plan_cost(n, P.W, P.c, P.W)) {
+      P.shared = true;
+      P.c = fb->c;
+      P.W = Ws;
+      P.stride = fb->n;
+      points = fb->table.as<G1Affine>();
+    }
+  }
+  finish_plan(P);
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
-  const int half = 1 << (P.c - 1);
 
   uint32_t *keys = (uint32_t *)ctx->msm_ws[0].ensure(sizeof(uint32_t) * total);
   uint32_t *vals = (uint32_t *)ctx->msm_ws[1].ensure(sizeof(uint32_t) * total);
@@ -346,17 +492,13 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
   G1Xyzz *buckets = (G1Xyzz *)ctx->msm_ws[5].ensure(sizeof(G1Xyzz) * P.nb);
   const size_t nchunks = (total + ACC_K - 1) / ACC_K;
   HeadTail *ht = (HeadTail *)ctx->msm_ws[6].ensure(sizeof(HeadTail) * nchunks);
-  const int red_l = half < RED_L ? half : RED_L;
-  const int groups = half / red_l;
-  G1Xyzz *parts = (G1Xyzz *)ctx->msm_ws[7].ensure(sizeof(G1Xyzz) * (size_t)P.W * groups);
-  G1Xyzz *wsum = (G1Xyzz *)ctx->msm_ws[8].ensure(sizeof(G1Xyzz) * P.W);
 
   {
     TNS_PROF(ctx, "msm_digits", 32.0 * n + 8.0 * total);
-    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, keys, vals);
+    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
+                                               keys, vals);
     TNS_LAUNCH_CHECK();
   }
-
   size_t temp_bytes = 0;
   TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total,
                                              0, P.end_bit, st));
@@ -365,28 +507,26 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
     TNS_PROF(ctx, "msm_sort", 16.0 * total);
     TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
                                                P.end_bit, st));
+    TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
+    k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
+    TNS_LAUNCH_CHECK();
   }
-
-  TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
-  k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
-  TNS_LAUNCH_CHECK();
   {
     TNS_PROF(ctx, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
     k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
                                                                    points, buckets, ht, nchunks);
     TNS_LAUNCH_CHECK();
   }
+  FixLevels F{};
   {
-    FixLevels F{};
-    size_t groups = nchunks / FIX_FAN;
-    size_t off = 0;
-    while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/32, /1024, ...
+    TNS_PROF(ctx, "msm_fixup", 0.0);
+    size_t groups = nchunks / FIX_FAN, off = 0;
+    while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/F, /F^2, ...
       F.len[F.n + 1] = groups;
       off += groups;
       groups /= FIX_FAN;
       F.n++;
     }
-    TNS_PROF(ctx, "msm_fixup", 0.0);
     if (F.n) {
       G1Xyzz *base = (G1Xyzz *)ctx->fix_ws.ensure(sizeof(G1Xyzz) * off);
       size_t o = 0;
@@ -401,32 +541,47 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n) {
     k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb);
     TNS_LAUNCH_CHECK();
   }
+  // bucket reduction (see the header): running sums over groups of L0 buckets, then
+  // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
+  // as nbits + 1 plain sums (the M_b and sum_g T_g) -- short dependency chains only
+  std::vector<G1Xyzz> fin;
+  const int L0 = (int)std::min<size_t>(RED_L, P.half);
+  const size_t g = P.half / L0;
+  int nbits = 0;
+  while (((size_t)1 << nbits) < g) nbits++;
+  const int specs = nbits + 1;
   {
     TNS_PROF(ctx, "msm_reduce", 128.0 * P.nb);
-    k_bucket_reduce<<<grid_for((size_t)P.W * groups, 64, 1u << 30), 64, 0, st>>>(buckets, P.W, half, red_l,
-                                                                                  parts);
+    G1Xyzz *T = (G1Xyzz *)ctx->msm_ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * g);
+    G1Xyzz *S = T + (size_t)P.Wr * g;
+    k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, L0, T, S);
     TNS_LAUNCH_CHECK();
-    // shrink groups per window 16x per pass (ping-pong in the bucket array) down to <= 256
-    G1Xyzz *src = parts, *dst = buckets;
-    int g = groups;
-    while (g > 256) {
-      const int chunk = 16;
-      const size_t n_out = (size_t)P.W * (g / chunk);
-      k_sum_chunks<<<grid_for(n_out, 64, 1u << 30), 64, 0, st>>>(src, n_out, chunk, dst);
-      TNS_LAUNCH_CHECK();
-      std::swap(src, dst);
-      g /= chunk;
-    }
-    k_window_sum<<<P.W, 256, 0, st>>>(src, g, wsum);
+    const int CH = (int)std::min<size_t>(16, g);
+    const size_t nch = g / CH;
+    const size_t nparts = (size_t)P.Wr * specs * nch;
+    G1Xyzz *parts = (G1Xyzz *)ctx->msm_ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * specs));
+    G1Xyzz *tmp = parts + nparts, *out = tmp + nparts;
+    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, nbits, CH, parts);
     TNS_LAUNCH_CHECK();
+    sum_sets(ctx, parts, P.Wr * specs, nch, tmp, out);
+    fin.resize((size_t)P.Wr * specs);
+    TNS_HIP(hipMemcpyAsync(fin.data(), out, sizeof(G1Xyzz) * fin.size(), hipMemcpyDeviceToHost, st));
+    TNS_HIP(hipStreamSynchronize(st));
   }
-  std::vector<G1Xyzz> S(P.W);
-  TNS_HIP(hipMemcpyAsync(S.data(), wsum, sizeof(G1Xyzz) * P.W, hipMemcpyDeviceToHost, st));
-  TNS_HIP(hipStreamSynchronize(st));
-  G1Xyzz acc = S[P.W - 1];
+  // R = sum_g T_g + L0 * sum_b 2^b M_b  (host: ~nbits + 4 doublings per set)
+  std::vector<G1Xyzz> Rw(P.Wr);
+  for (int r = 0; r < P.Wr; r++) {
+    const G1Xyzz *f = &fin[(size_t)r * specs];
+    G1Xyzz acc = G1Xyzz::inf();
+    for (int b = nbits - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), f[b]);
+    for (int L = L0; L > 1; L >>= 1) acc = xyzz_dbl(acc);
+    Rw[r] = xyzz_add(f[nbits], acc);
+  }
+  if (P.shared) return Rw[0];
+  G1Xyzz acc = Rw[P.W - 1];
   for (int w = P.W - 2; w >= 0; w--) {
     for (int k = 0; k < P.c; k++) acc = xyzz_dbl(acc);
-    acc = xyzz_add(acc, S[w]);
+    acc = xyzz_add(acc, Rw[w]);
   }
   return acc;
 }

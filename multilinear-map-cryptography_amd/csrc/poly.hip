@@ -174,6 +174,13 @@ __global__ void __launch_bounds__(256) k_batch_to_affine(const G1Xyzz *__restric
   }
 }
 
+void xyzz_to_affine_batch_dev(Ctx *c, const G1Xyzz *in, size_t n, G1Affine *out, Fq *prefix) {
+  if (!n) return;
+  size_t bchunks = (n + BATCH_INV_CHUNK - 1) / BATCH_INV_CHUNK;
+  k_batch_to_affine<<<grid_for(bchunks, 256, 1u << 30), 256, 0, c->stream>>>(in, n, prefix, out);
+  TNS_LAUNCH_CHECK();
+}
+
 // host: d * 2^(8w) * G for w < 32, d < 256 (d = 0 -> identity), affine
 static std::vector<G1Affine> build_fixed_base_table() {
   std::vector<G1Xyzz> tab(32 * 256);

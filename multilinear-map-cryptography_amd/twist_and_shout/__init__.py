@@ -146,6 +146,11 @@ class Context:
         when it has tau; False: vector_to_polynomial + coefficient KZG.  Same proofs."""
         _check(N.load().tns_ctx_set_commit_basis(self.handle, 1 if lagrange else 0))
 
+    def set_msm_tables(self, on: bool):
+        """True (default): MSMs over fixed bases use their window tables (one shared bucket
+        set); False: per-window buckets.  Same results."""
+        _check(N.load().tns_ctx_set_msm_tables(self.handle, 1 if on else 0))
+
     def timing(self):
         out = (C.c_double * 6)()
         N.load().tns_last_prove_timing(self.handle, out)

@@ -145,6 +145,23 @@ def test_msm_skewed_scalars_large(pattern):
     assert got == po.affine_mul(po.G1_GEN, s)
 
 
+@pytest.mark.parametrize("logn", [16, 20])
+def test_msm_window_tables_equal_per_window_layout(logn):
+    """Shared-bucket MSM (fixed-base window table) == per-window MSM, full-width and
+    narrow scalars."""
+    pp, _ = params(logn - 2)
+    n = 1 << logn
+    ctx = ts.Context.get(0)
+    for c in (rand_fr_mont(n, seed=logn + 1), ts.to_mont([i * 7919 % (1 << 40) for i in range(n)])):
+        a = ts.msm(pp.commitment_params, c)
+        ctx.set_msm_tables(False)
+        try:
+            b = ts.msm(pp.commitment_params, c)
+        finally:
+            ctx.set_msm_tables(True)
+        assert a == b
+
+
 def test_commit_beyond_srs_is_commitment_error():
     pp, _ = params(1)  # 9 SRS points
     with pytest.raises(ts.CommitmentError):
