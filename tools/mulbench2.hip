@@ -1,0 +1,257 @@
+// mulbench2.hip -- throughput of 256-bit Montgomery multiplication variants on gfx950, alone
+// and inside the XYZZ mixed addition that dominates the MSM.
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/mulbench2.hip -o tools/mulbench2
+//
+// Variants (product scanning, 8 x u32 limbs, carry of the 64-bit column accumulator kept
+// in a 32-bit overflow word):
+//   0: current library mul (carry through vcc)
+//   1: carry through an allocatable SGPR pair (independent chains may interleave)
+//   2: two column accumulators (even / odd products) merged per column: 2x ILP
+//   3: peak: independent v_mad_u64_u32 streams (no data dependency) -- the VALU ceiling
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../multilinear-map-cryptography_amd/csrc/bn254.hpp"
+using namespace tns;
+typedef unsigned long long ull;
+
+#define MAC_S(acc, c2, x, y)                                                                         \
+  do {                                                                                               \
+    ull _cc;                                                                                         \
+    asm("v_mad_u64_u32 %0, %2, %3, %4, %0\n\tv_addc_co_u32_e64 %1, %2, 0, %1, %2"                 \
+        : "+v"(acc), "+v"(c2), "=&s"(_cc)                                                           \
+        : "v"(x), "v"(y));                                                                           \
+  } while (0)
+
+template <class C>
+__device__ __forceinline__ Fp<C> mul_sgpr(const Fp<C> &a, const Fp<C> &b) {
+  u32 m[8], r[8];
+  ull acc = 0;
+  u32 c2 = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+#pragma unroll
+    for (int i = 0; i <= k; i++) MAC_S(acc, c2, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = 0; i < k; i++) MAC_S(acc, c2, m[i], C::M[k - i]);
+    m[k] = (u32)acc * C::INV;
+    MAC_S(acc, c2, m[k], C::M[0]);
+    acc = (acc >> 32) | ((ull)c2 << 32);
+    c2 = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+#pragma unroll
+    for (int i = k - 7; i <= 7; i++) MAC_S(acc, c2, a.v[i], b.v[k - i]);
+#pragma unroll
+    for (int i = k - 7; i <= 7; i++) MAC_S(acc, c2, m[i], C::M[k - i]);
+    r[k - 8] = (u32)acc;
+    acc = (acc >> 32) | ((ull)c2 << 32);
+    c2 = 0;
+  }
+  r[7] = (u32)acc;
+  Fp<C> o;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.v[i] = r[i];
+  reduce_once(o);
+  return o;
+}
+
+// two accumulators: products alternate between (acc0, c0) and (acc1, c1); merged per column
+template <class C>
+__device__ __forceinline__ Fp<C> mul_dual(const Fp<C> &a, const Fp<C> &b) {
+  u32 m[8], r[8];
+  ull acc0 = 0, acc1 = 0;
+  u32 c0 = 0, c1 = 0;
+  auto merge = [&]() {
+    // acc0 += acc1 (64-bit) with carries into c0
+    ull s = acc0 + acc1;
+    c0 += c1 + (s < acc0 ? 1u : 0u);
+    acc0 = s;
+    acc1 = 0;
+    c1 = 0;
+  };
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i <= k; i++, t++) {
+      if (t & 1) MAC_S(acc1, c1, a.v[i], b.v[k - i]);
+      else MAC_S(acc0, c0, a.v[i], b.v[k - i]);
+    }
+#pragma unroll
+    for (int i = 0; i < k; i++, t++) {
+      if (t & 1) MAC_S(acc1, c1, m[i], C::M[k - i]);
+      else MAC_S(acc0, c0, m[i], C::M[k - i]);
+    }
+    merge();
+    m[k] = (u32)acc0 * C::INV;
+    MAC_S(acc0, c0, m[k], C::M[0]);
+    acc0 = (acc0 >> 32) | ((ull)c0 << 32);
+    c0 = 0;
+  }
+#pragma unroll
+  for (int k = 8; k < 15; k++) {
+    int t = 0;
+#pragma unroll
+    for (int i = k - 7; i <= 7; i++, t++) {
+      if (t & 1) MAC_S(acc1, c1, a.v[i], b.v[k - i]);
+      else MAC_S(acc0, c0, a.v[i], b.v[k - i]);
+    }
+#pragma unroll
+    for (int i = k - 7; i <= 7; i++, t++) {
+      if (t & 1) MAC_S(acc1, c1, m[i], C::M[k - i]);
+      else MAC_S(acc0, c0, m[i], C::M[k - i]);
+    }
+    merge();
+    r[k - 8] = (u32)acc0;
+    acc0 = (acc0 >> 32) | ((ull)c0 << 32);
+    c0 = 0;
+  }
+  r[7] = (u32)acc0;
+  Fp<C> o;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o.v[i] = r[i];
+  reduce_once(o);
+  return o;
+}
+
+template <int V>
+__device__ __forceinline__ Fq M(const Fq &a, const Fq &b) {
+  if (V == 0) return mul(a, b);
+  if (V == 1) return mul_sgpr(a, b);
+  return mul_dual(a, b);
+}
+
+// madd-2008-s with the variant multiply (no special cases: benchmark only)
+template <int V>
+__device__ __forceinline__ G1Xyzz madd_v(const G1Xyzz &p, const G1Affine &q) {
+  Fq U2 = M<V>(q.x, p.zz), S2 = M<V>(q.y, p.zzz);
+  Fq P = sub(U2, p.x), R = sub(S2, p.y);
+  Fq PP = M<V>(P, P), PPP = M<V>(P, PP), Q = M<V>(p.x, PP);
+  G1Xyzz r;
+  r.x = sub(sub(M<V>(R, R), PPP), dbl(Q));
+  r.y = sub(M<V>(R, sub(Q, r.x)), M<V>(p.y, PPP));
+  r.zz = M<V>(p.zz, PP);
+  r.zzz = M<V>(p.zzz, PPP);
+  return r;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) k_mul(Fq *x, int iters) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  Fq a = x[2 * i], b = x[2 * i + 1];
+  for (int k = 0; k < iters; k++) a = M<V>(a, b);
+  x[2 * i] = a;
+}
+
+template <int V>
+__global__ void __launch_bounds__(256) k_madd(G1Xyzz *acc_io, const G1Affine *pts, int iters, int npts) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  G1Xyzz acc = acc_io[i];
+  for (int k = 0; k < iters; k++) acc = madd_v<V>(acc, pts[(i * 7 + k * 131) & (npts - 1)]);
+  acc_io[i] = acc;
+}
+
+__global__ void __launch_bounds__(256) k_peak(u32 *x, int iters) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  u32 a = x[i], b = x[i + 1];
+  ull s0 = a, s1 = b, s2 = a ^ 1, s3 = b ^ 3, s4 = a + 5, s5 = b + 7, s6 = a * 3, s7 = b * 5;
+  for (int k = 0; k < iters; k++) {
+#define P1(s) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(s) : "v"(a), "v"(b) : "vcc")
+    P1(s0); P1(s1); P1(s2); P1(s3); P1(s4); P1(s5); P1(s6); P1(s7);
+  }
+  x[i] = (u32)(s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7);
+}
+
+__global__ void k_check(const Fq *x, int n, unsigned *bad) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Fq a = x[2 * i], b = x[2 * i + 1];
+  Fq p = mul(a, b);
+  if (!(mul_sgpr(a, b) == p) || !(mul_dual(a, b) == p)) atomicAdd(bad, 1u);
+}
+
+static float time_ms(void (*launch)(void *), void *arg) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  launch(arg);
+  hipEventRecord(e0);
+  launch(arg);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  return ms;
+}
+
+struct Args {
+  void *p, *q;
+  int blocks, iters, npts;
+};
+template <int V>
+static void L_mul(void *a) {
+  Args *A = (Args *)a;
+  k_mul<V><<<A->blocks, 256>>>((Fq *)A->p, A->iters);
+}
+template <int V>
+static void L_madd(void *a) {
+  Args *A = (Args *)a;
+  k_madd<V><<<A->blocks, 256>>>((G1Xyzz *)A->p, (const G1Affine *)A->q, A->iters, A->npts);
+}
+static void L_peak(void *a) {
+  Args *A = (Args *)a;
+  k_peak<<<A->blocks, 256>>>((u32 *)A->p, A->iters);
+}
+
+int main() {
+  const int blocks = 256 * 8 * 2;
+  const size_t n = (size_t)blocks * 256;
+  std::vector<Fq> h(2 * n);
+  uint64_t s = 88172645463325252ULL;
+  for (auto &e : h) {
+    for (int k = 0; k < 8; k++) {
+      s ^= s << 13;
+      s ^= s >> 7;
+      s ^= s << 17;
+      e.v[k] = (u32)s;
+    }
+    e.v[7] &= 0x0fffffff;
+  }
+  Fq *d;
+  hipMalloc(&d, sizeof(Fq) * 2 * n + 64);
+  hipMemcpy(d, h.data(), sizeof(Fq) * 2 * n, hipMemcpyHostToDevice);
+  unsigned *bad;
+  hipMalloc(&bad, 4);
+  hipMemset(bad, 0, 4);
+  k_check<<<(n + 255) / 256, 256>>>(d, (int)n, bad);
+  unsigned hb = 0;
+  hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
+  printf("variant mismatches vs library mul: %u of %zu\n", hb, n);
+
+  Args A{d, nullptr, blocks, 100, 0};
+  const double muls = (double)n * A.iters;
+  float t0 = time_ms(L_mul<0>, &A), t1 = time_ms(L_mul<1>, &A), t2 = time_ms(L_mul<2>, &A);
+  printf("mul chain   : vcc %.1f  sgpr %.1f  dual %.1f  G mul/s\n", muls / t0 / 1e6, muls / t1 / 1e6, muls / t2 / 1e6);
+  A.iters = 2000;
+  float tp = time_ms(L_peak, &A);
+  printf("peak v_mad_u64_u32: %.2f T mad/s (independent streams)\n", (double)n * A.iters * 8 / tp / 1e9);
+
+  // madd over a 64 MiB random point table
+  const int npts = 1 << 20;
+  G1Affine *pts;
+  hipMalloc(&pts, sizeof(G1Affine) * npts);
+  hipMemcpy(pts, h.data(), sizeof(G1Affine) * npts, hipMemcpyHostToDevice);
+  G1Xyzz *accs;
+  hipMalloc(&accs, sizeof(G1Xyzz) * n);
+  hipMemcpy(accs, h.data(), sizeof(G1Xyzz) * n / 2, hipMemcpyHostToDevice);
+  A = Args{accs, pts, blocks, 20, npts};
+  const double madds = (double)n * A.iters;
+  float m0 = time_ms(L_madd<0>, &A), m1 = time_ms(L_madd<1>, &A), m2 = time_ms(L_madd<2>, &A);
+  printf("madd        : vcc %.2f  sgpr %.2f  dual %.2f  G madd/s\n", madds / m0 / 1e6, madds / m1 / 1e6,
+         madds / m2 / 1e6);
+  return 0;
+}
