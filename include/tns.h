@@ -211,6 +211,44 @@ int tns_shout_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *p
 int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, size_t n,
                    uint64_t out_proj[12]);
 
+/* ---------------------------------------------------------------- one proof across GPUs
+ * SURVEY 8(e) / BASELINE C5: the evaluation vectors and the SRS of ONE Twist/Shout proof
+ * sharded over `size` ranks (one process -- or one tns_ctx -- per GPU).  Rank r holds the
+ * contiguous slice [r N/size, (r+1) N/size) of the padded length-N vectors and the matching
+ * slice of the Lagrange basis; the exchange steps are allgathers of partial MSM sums,
+ * barycentric partials and one folded value per MLE table (a few hundred bytes per step).
+ * Every rank returns the same proof, identical to the unsharded prover's.  size must be a
+ * power of two <= N; the SRS must carry tau (setup_params / tns_srs_set_tau). */
+typedef struct tns_comm tns_comm;
+/* allgather: place every rank's `bytes` from `send`, in rank order, into `recv`
+ * (size * bytes); return 0 on success. */
+typedef int (*tns_allgather_fn)(void *user, const void *send, size_t bytes, void *recv);
+/* RCCL communicator (ncclAllGather on the context's stream).  Rank 0 calls
+ * tns_comm_unique_id and the launcher broadcasts the 128 bytes. */
+int tns_comm_unique_id(uint8_t uid[128]);
+int tns_comm_create(tns_ctx *ctx, int rank, int size, const uint8_t uid[128], tns_comm **out);
+/* Communicator over any host-side transport. */
+int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user, tns_comm **out);
+void tns_comm_destroy(tns_comm *comm);
+/* setup_params for rank `rank` of `size`: the same params/tau as tns_setup_params, with the
+ * SRS holding only its contiguous share of g1_powers (the "SRS shard generated locally from
+ * tau"); tns_srs_len still reports the full length. */
+int tns_setup_params_shard(tns_ctx *ctx, unsigned log_size, int rank, int size, tns_params *out,
+                           tns_srs **srs_out);
+/* Twist::prove of a trace of n_total operations whose operations
+ * [rank * N/size, rank * N/size + n_local) (N = next_pow2(n_total)) this rank holds on the
+ * device; n_local must be that slice's length (0 for ranks past the end). */
+int tns_twist_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, tns_comm *comm,
+                            const uint64_t *d_addr, const uint64_t *d_value, const uint8_t *d_is_write,
+                            size_t n_local, uint64_t n_total, tns_proof *out);
+/* Shout::prove with the table (n_entries_total, padded T) and the lookup indices
+ * (n_lookups_total, padded M) sliced the same way: entries [rank*T/size, +n_entries_local),
+ * indices [rank*M/size, +n_lookups_local). */
+int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, tns_comm *comm,
+                            const uint64_t *d_entries, size_t n_entries_local, uint64_t n_entries_total,
+                            const uint64_t *d_indices, size_t n_lookups_local, uint64_t n_lookups_total,
+                            tns_proof *out);
+
 /* ---------------------------------------------------------------- kernel timing */
 /* HIP-event timing of the named stages on the context stream ("msm_accumulate",
  * "msm_sort", "msm_digits", "msm_reduce", "ntt_stage", "ntt_lds", "ntt_pointwise",
@@ -233,6 +271,10 @@ void tns_fr_rand_batch(const uint8_t seed[32], size_t n, uint64_t *out_mont);
  * and records the current memory value.  value_u64 holds the values as integers. */
 int tns_bench_trace(size_t memory_size, size_t n_ops, uint64_t *addr, uint64_t *value_u64,
                     uint8_t *is_write);
+/* Operations [first, first + count) of the n_total-operation ProtocolBenchmarks trace (the
+ * memory state is replayed from operation 0): one rank's slice of a sharded trace. */
+int tns_bench_trace_slice(size_t memory_size, uint64_t n_total, uint64_t first, size_t count, uint64_t *addr,
+                          uint64_t *value, uint8_t *is_write);
 
 /* Wall-clock breakdown of the last prove on this context (milliseconds):
  * [0] H2D, [1] interpolation, [2] commit MSMs, [3] sum-check, [4] open, [5] total. */

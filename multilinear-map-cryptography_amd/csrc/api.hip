@@ -25,6 +25,10 @@ struct tns_srs {
 struct tns_transcript {
   tns::HostTranscript t;
 };
+struct tns_comm {
+  tns::Comm *c = nullptr;
+  ~tns_comm() { delete c; }
+};
 struct tns_buffer {
   tns::DevBuf buf;
   size_t bytes = 0;
@@ -84,6 +88,8 @@ struct Timer {
 // KZGCommitment::commit on device-resident coefficients (src/commitments.rs:162-180)
 static G1Affine commit_dev(Ctx *c, const Srs &srs, const Fr *coeffs, size_t n) {
   if (n > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+  if (srs.first != 0 || srs.held < n)
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "coefficient commitments need the whole SRS (this is a shard)");
   return xyzz_to_affine(msm_dev(c, srs.points.as<G1Affine>(), coeffs, n, srs_fixed_base(c, srs, n)));
 }
 
@@ -103,39 +109,70 @@ static void open_dev(Ctx *c, const Srs &srs, const Fr *coeffs, size_t n, const F
 }
 
 // One committed vector of Twist/Shout::prove: evaluations y on the nodes 0..N-1
-// (vector_to_polynomial input, src/polynomials.rs:248-262).  Committed and opened via
-// the Lagrange basis when the SRS provides it, else via interpolated coefficients.
+// (vector_to_polynomial input, src/polynomials.rs:248-262), of which this rank holds the
+// slice [first, first + cnt).  Committed and opened via the Lagrange basis when the SRS
+// provides it (partial MSMs summed over the ranks), else via interpolated coefficients.
 struct EvalPoly {
-  const Fr *y = nullptr;       // device, N (must stay intact until opened)
-  Fr *coeffs = nullptr;        // device scratch, N (coefficient path)
-  size_t N = 0;
+  const Fr *y = nullptr;       // device, cnt (must stay intact until opened)
+  Fr *coeffs = nullptr;        // device scratch, N (coefficient path, unsharded only)
+  size_t N = 0, first = 0, cnt = 0;
   const LagrangeBasis *basis = nullptr;
   bool have_coeffs = false;
 };
 
-static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p) {
+static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p, Comm &m) {
   if (p.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
-  p.basis = lagrange_basis_dev(c, srs, p.N);
-  if (p.basis) return xyzz_to_affine(msm_dev(c, p.basis->points.as<G1Affine>(), p.y, p.N, p.basis->fb));
+  p.basis = lagrange_basis_dev(c, srs, p.N, p.first, p.cnt);
+  if (p.basis) {
+    const G1Xyzz part = msm_dev(c, p.basis->points.as<G1Affine>(), p.y, p.cnt, p.basis->fb);
+    return xyzz_to_affine(allgather_sum_g1(c, m, part));
+  }
+  if (m.size > 1) throw Error(TNS_ERR_INVALID_PARAMETERS, "sharded proving needs an SRS with tau (Lagrange basis)");
   interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
   p.have_coeffs = true;
   return commit_dev(c, srs, p.coeffs, p.N);
 }
 
 static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *value, G1Affine *proof,
-                       DevBuf &sbuf) {
-  if (p.basis) {
-    Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.N);
-    if (lagrange_quotient_dev(c, p.y, p.N, z, value, q)) {
-      *proof = xyzz_to_affine(msm_dev(c, p.basis->points.as<G1Affine>(), q, p.N, p.basis->fb));
-      return;
+                       DevBuf &sbuf, Comm &m) {
+  if (p.basis && !fr_is_node(z, p.N)) {
+    Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.cnt);
+    Fr part[2];
+    lagrange_open_partial_dev(c, p.y, p.N, p.first, p.cnt, z, q, &part[0], &part[1]);
+    Fr ell = Fr::one(), S = Fr::zero();
+    if (m.size == 1) {
+      ell = part[0];
+      S = part[1];
+    } else {
+      const std::vector<Fr> all = allgather_fr(c, m, part, 2);
+      for (int r = 0; r < m.size; r++) {
+        ell = mul(ell, all[2 * r]);
+        S = add(S, all[2 * r + 1]);
+      }
     }
+    *value = mul(ell, S);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
+    lagrange_quotient_finish_dev(c, p.y, p.cnt, *value, q);
+    const G1Xyzz pp = msm_dev(c, p.basis->points.as<G1Affine>(), q, p.cnt, p.basis->fb);
+    *proof = xyzz_to_affine(allgather_sum_g1(c, m, pp));
+    return;
   }
+  if (m.size > 1)  // z on a node: probability ~2^-230; the coefficient route is unsharded
+    throw Error(TNS_ERR_PROOF_GENERATION, "opening challenge is an interpolation node (sharded prover)");
   if (!p.have_coeffs) {  // z is a node (or no basis): coefficient form
     interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
     p.have_coeffs = true;
   }
   open_dev(c, srs, p.coeffs, p.N, z, value, proof, sbuf);
+}
+
+// shard geometry: `size` ranks over N padded entries (size a power of two <= N)
+static void check_shard(const Comm &m, size_t N, const char *what) {
+  if (m.size & (m.size - 1)) throw Error(TNS_ERR_INVALID_PARAMETERS, "rank count must be a power of two");
+  if ((size_t)m.size > N)
+    throw Error(TNS_ERR_INVALID_PARAMETERS, std::string("more ranks than padded ") + what + " entries");
+}
+static size_t slice_count(uint64_t n_total, size_t first, size_t L) {
+  return n_total <= first ? 0 : (size_t)std::min<uint64_t>(L, n_total - first);
 }
 
 // multi-threaded element-wise host conversion
@@ -205,34 +242,51 @@ int tns_ctx_synchronize(tns_ctx *ctx) {
   });
 }
 
+// setup_params (src/utils.rs:79-131) for ranks [rank] of [size]: the SRS holds the
+// contiguous share [first, first + held) of the num_powers g1_powers (all of them for size 1)
+static void setup_core(tns_ctx *ctx, unsigned log_size, int rank, int size, tns_params *out, tns_srs **srs_out) {
+  if (log_size > 26) throw Error(TNS_ERR_INVALID_PARAMETERS, "log_size too large");
+  if (size < 1 || rank < 0 || rank >= size) throw Error(TNS_ERR_INVALID_PARAMETERS, "bad shard");
+  std::memset(out, 0, sizeof *out);
+  out->log_size = log_size;
+  out->max_operations = (uint64_t)1 << (log_size + 2);  // src/utils.rs:80
+  out->num_powers = next_pow2(out->max_operations) + 1;  // src/utils.rs:89
+  uint8_t seed42[32];
+  std::memset(seed42, 42, 32);
+  Fr tau = host_fr_rand_chacha(seed42, out->fiat_shamir_seed);  // src/utils.rs:81-84, 101-102
+  std::memcpy(out->tau, &tau, 32);
+  if (!srs_out) return;
+  *srs_out = nullptr;
+  CtxScope g(&ctx->c);
+  tns_srs *s = new tns_srs();
+  s->s.device = ctx->c.device;
+  s->s.n = out->num_powers;
+  const size_t base = s->s.n / size, rem = s->s.n % size;
+  s->s.first = (size_t)rank * base + std::min<size_t>(rank, rem);
+  s->s.held = base + ((size_t)rank < rem ? 1 : 0);
+  s->s.has_tau = true;
+  s->s.tau = tau;
+  try {
+    G1Affine *pts = (G1Affine *)s->s.points.ensure(sizeof(G1Affine) * (s->s.held ? s->s.held : 1));
+    srs_generate_dev(&ctx->c, tau, s->s.first, s->s.held, pts);
+  } catch (...) {
+    delete s;
+    throw;
+  }
+  *srs_out = s;
+}
+
 int tns_setup_params(tns_ctx *ctx, unsigned log_size, tns_params *out, tns_srs **srs_out) {
   return guarded([&]() {
-    if (log_size > 26) throw Error(TNS_ERR_INVALID_PARAMETERS, "log_size too large");
-    std::memset(out, 0, sizeof *out);
-    out->log_size = log_size;
-    out->max_operations = (uint64_t)1 << (log_size + 2);  // src/utils.rs:80
-    out->num_powers = next_pow2(out->max_operations) + 1;  // src/utils.rs:89
-    uint8_t seed42[32];
-    std::memset(seed42, 42, 32);
-    Fr tau = host_fr_rand_chacha(seed42, out->fiat_shamir_seed);  // src/utils.rs:81-84, 101-102
-    std::memcpy(out->tau, &tau, 32);
-    if (srs_out) {
-      *srs_out = nullptr;
-      CtxScope g(&ctx->c);
-      tns_srs *s = new tns_srs();
-      s->s.device = ctx->c.device;
-      s->s.n = out->num_powers;
-      s->s.has_tau = true;
-      s->s.tau = tau;
-      try {
-        G1Affine *pts = (G1Affine *)s->s.points.ensure(sizeof(G1Affine) * s->s.n);
-        srs_generate_dev(&ctx->c, tau, s->s.n, pts);
-      } catch (...) {
-        delete s;
-        throw;
-      }
-      *srs_out = s;
-    }
+    setup_core(ctx, log_size, 0, 1, out, srs_out);
+    return TNS_OK;
+  });
+}
+
+int tns_setup_params_shard(tns_ctx *ctx, unsigned log_size, int rank, int size, tns_params *out,
+                           tns_srs **srs_out) {
+  return guarded([&]() {
+    setup_core(ctx, log_size, rank, size, out, srs_out);
     return TNS_OK;
   });
 }
@@ -243,6 +297,7 @@ int tns_srs_upload(tns_ctx *ctx, const uint64_t *g1, size_t n, tns_srs **out) {
     tns_srs *s = new tns_srs();
     s->s.device = ctx->c.device;
     s->s.n = n;
+    s->s.held = n;
     try {
       void *p = s->s.points.ensure(sizeof(G1Affine) * (n ? n : 1));
       if (n) TNS_HIP(hipMemcpy(p, g1, sizeof(G1Affine) * n, hipMemcpyHostToDevice));
@@ -258,7 +313,7 @@ int tns_srs_upload(tns_ctx *ctx, const uint64_t *g1, size_t n, tns_srs **out) {
 int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_out, size_t n) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
-    if (n > srs->s.n) throw Error(TNS_ERR_INVALID_PARAMETERS, "download beyond SRS length");
+    if (srs->s.first != 0 || n > srs->s.held) throw Error(TNS_ERR_INVALID_PARAMETERS, "download beyond SRS length");
     if (n) TNS_HIP(hipMemcpy(g1_out, srs->s.points.p, sizeof(G1Affine) * n, hipMemcpyDeviceToHost));
     return TNS_OK;
   });
@@ -286,7 +341,7 @@ int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n) {
     if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
     const bool saved = ctx->c.lagrange_commit;
     ctx->c.lagrange_commit = true;
-    const LagrangeBasis *b = lagrange_basis_dev(&ctx->c, srs->s, n);
+    const LagrangeBasis *b = lagrange_basis_dev(&ctx->c, srs->s, n, 0, n);
     ctx->c.lagrange_commit = saved;
     (void)b;  // nullptr only when tau is itself a node: the coefficient path is used then
     return TNS_OK;
@@ -332,6 +387,8 @@ static void upload_evals(tns_ctx *ctx, const uint64_t *evals, size_t n, DevBuf &
   TNS_HIP(hipMemcpyAsync(dy, evals, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
   p.y = dy;
   p.N = n;
+  p.first = 0;
+  p.cnt = n;
   p.coeffs = (Fr *)cf.ensure(sizeof(Fr) * n);
 }
 
@@ -341,7 +398,7 @@ int tns_kzg_commit_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals
     DevBuf d, cf;
     EvalPoly p;
     upload_evals(ctx, evals, n, d, cf, p);
-    store_proj(commit_evals(&ctx->c, srs->s, p), out);
+    store_proj(commit_evals(&ctx->c, srs->s, p, comm_self()), out);
     return TNS_OK;
   });
 }
@@ -354,11 +411,11 @@ int tns_kzg_open_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, 
     EvalPoly p;
     upload_evals(ctx, evals, n, d, cf, p);
     if (n > srs->s.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
-    p.basis = lagrange_basis_dev(&ctx->c, srs->s, n);
+    p.basis = lagrange_basis_dev(&ctx->c, srs->s, n, 0, n);
     Fr zz, v;
     std::memcpy(&zz, z, 32);
     G1Affine pi;
-    open_evals(&ctx->c, srs->s, p, zz, &v, &pi, s);
+    open_evals(&ctx->c, srs->s, p, zz, &v, &pi, s, comm_self());
     std::memcpy(value, &v, 32);
     store_proj(pi, proof);
     return TNS_OK;
@@ -509,14 +566,47 @@ int tns_last_prove_timing(tns_ctx *ctx, double out_ms[6]) {
 }
 
 // ---------------------------------------------------------------- protocols
+// Sum-check over the (zero) constraint closure + the two openings, for the rank's slices.
+// The first nv - log2(size) rounds bind variables inside every slice (LSB-first,
+// src/polynomials.rs:111-119), so they run locally; the last log2(size) rounds run on
+// the host over the one folded value per table and rank (allgathered).
 static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *const *mles, int n_mles,
                              unsigned nv, EvalPoly &polyA, EvalPoly &polyB, tns_proof *out, double *timing,
-                             DevBuf &sbuf) {
+                             DevBuf &sbuf, Comm &m) {
   Timer t_sc;
+  unsigned lr = 0;
+  while ((1 << lr) < m.size) lr++;
+  const unsigned nv_loc = nv - lr;  // check_shard guarantees size <= 2^nv
   std::vector<Fr> rounds(4 * (size_t)(nv ? nv : 1)), chal(nv ? nv : 1);
   Fr finals[4], fe;
   // zero constraint closure (src/twist.rs:186-214, src/shout.rs:160-184): no terms
-  sumcheck_prove_dev(c, mles, n_mles, nv, Fr::zero(), nullptr, 0, tr, rounds.data(), chal.data(), finals, &fe);
+  sumcheck_prove_dev(c, mles, n_mles, nv_loc, Fr::zero(), nullptr, 0, tr, rounds.data(), chal.data(), finals, &fe);
+  if (lr) {
+    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles);  // rank-major
+    std::vector<std::vector<Fr>> tab(n_mles, std::vector<Fr>(m.size));
+    for (int r = 0; r < m.size; r++)
+      for (int j = 0; j < n_mles; j++) tab[j][r] = all[(size_t)r * n_mles + j];
+    char lab[64];
+    for (unsigned rnd = nv_loc; rnd < nv; rnd++) {
+      // round polynomial of the zero closure: [0, 0, 0, 0] (src/sumcheck.rs:77-96)
+      snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd);
+      tr.append_label(lab);
+      for (int x = 0; x < 4; x++) {
+        rounds[4 * rnd + x] = Fr::zero();
+        tr.append_fr(Fr::zero());
+      }
+      snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
+      const Fr ch = tr.challenge(lab);
+      chal[rnd] = ch;
+      for (auto &t : tab) {  // T'[s] = T[2s] + r (T[2s+1] - T[2s])
+        const size_t h = t.size() / 2;
+        for (size_t q = 0; q < h; q++) t[q] = add(t[2 * q], mul(ch, sub(t[2 * q + 1], t[2 * q])));
+        t.resize(h);
+      }
+    }
+    for (int j = 0; j < n_mles; j++) finals[j] = tab[j][0];
+    fe = Fr::zero();  // the closure is identically zero
+  }
   out->num_rounds = nv;
   std::memcpy(out->round_polynomials, rounds.data(), 128 * (size_t)nv);
   std::memcpy(out->sumcheck_challenges, chal.data(), 32 * (size_t)nv);
@@ -535,8 +625,8 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     std::memcpy(out->opening_point, &z, 32);
     Fr va, vb;
     G1Affine pa, pb;
-    open_evals(c, srs, polyA, z, &va, &pa, sbuf);
-    open_evals(c, srs, polyB, z, &vb, &pb, sbuf);
+    open_evals(c, srs, polyA, z, &va, &pa, sbuf, m);
+    open_evals(c, srs, polyB, z, &vb, &pb, sbuf, m);
     store_proj(pa, out->opening_proofs[0]);
     store_proj(pb, out->opening_proofs[1]);
     std::memcpy(out->final_evaluations[0], &va, 32);
@@ -557,20 +647,26 @@ __global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, ui
     if (idx[i] >= bound) *bad = 1;
 }
 
-// Twist::prove (src/twist.rs:107-252).  kind: where addr/value/is_write live (H2D or D2D).
-static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *addr,
-                       const uint64_t *value, const uint8_t *is_write, size_t n_ops, tns_proof *out,
-                       hipMemcpyKind kind) {
+// Twist::prove (src/twist.rs:107-252) for this rank's slice of the trace: operations
+// [rank L, rank L + n_local) of n_total, L = next_pow2(n_total) / size.  kind: where
+// addr/value/is_write live (H2D or D2D).  size 1 = the unsharded prover.
+static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, Comm &m, const uint64_t *addr,
+                       const uint64_t *value, const uint8_t *is_write, size_t n_ops, uint64_t n_total,
+                       tns_proof *out, hipMemcpyKind kind) {
   Timer total;
   CtxScope g(&ctx->c);
   Ctx *c = &ctx->c;
   hipStream_t st = c->stream;
   std::memset(out, 0, sizeof *out);
-  if (n_ops > params->max_operations)  // src/twist.rs:108-112
+  if (n_total > params->max_operations)  // src/twist.rs:108-112
     throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many operations");
-  const size_t N = next_pow2(n_ops);  // :141 next_power_of_two().max(1)
+  const size_t N = next_pow2(n_total);  // :141 next_power_of_two().max(1)
   const unsigned nv = ilog2_exact(N);
   if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "trace too long");
+  check_shard(m, N, "trace");
+  const size_t L = N / m.size, first = (size_t)m.rank * L;
+  if (n_ops != slice_count(n_total, first, L))
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "local operation count does not match this rank's slice");
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
   // ---- SoA extraction / padding into the resident workspace (src/twist.rs:115-148)
@@ -578,7 +674,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
          &d_v = c->prove_ws[3], &d_o = c->prove_ws[4], &d_ca = c->prove_ws[5], &d_cv = c->prove_ws[6],
          &d_s = c->prove_ws[7];
-  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * N), *V = (Fr *)d_v.ensure(sizeof(Fr) * N), *O = (Fr *)d_o.ensure(sizeof(Fr) * N);
+  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * L), *V = (Fr *)d_v.ensure(sizeof(Fr) * L), *O = (Fr *)d_o.ensure(sizeof(Fr) * L);
   const uint64_t *ar = addr;
   const uint8_t *fl = is_write;
   if (kind == hipMemcpyHostToDevice) {
@@ -592,10 +688,10 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     fl = dfl;
   }
   if (n_ops) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
-  fr_fill_zero_dev(c, A, N);
+  fr_fill_zero_dev(c, A, L);
   to_mont_u64_dev(c, ar, A, n_ops);
-  if (N > n_ops) fr_fill_zero_dev(c, V + n_ops, N - n_ops);
-  k_write_flags<<<grid_for(N, 256), 256, 0, st>>>(fl, O, n_ops, N);
+  if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
+  k_write_flags<<<grid_for(L, 256), 256, 0, st>>>(fl, O, n_ops, L);
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
@@ -604,17 +700,19 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   Timer t_int;
   EvalPoly pa, pv;
   pa.N = pv.N = N;
-  pa.coeffs = (Fr *)d_ca.ensure(sizeof(Fr) * N);
-  pv.coeffs = (Fr *)d_cv.ensure(sizeof(Fr) * N);
-  Fr *YA = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * N), *YV = (Fr *)c->prove_ws[9].ensure(sizeof(Fr) * N);
-  TNS_HIP(hipMemcpyAsync(YA, A, sizeof(Fr) * N, hipMemcpyDeviceToDevice, st));
-  TNS_HIP(hipMemcpyAsync(YV, V, sizeof(Fr) * N, hipMemcpyDeviceToDevice, st));
+  pa.first = pv.first = first;
+  pa.cnt = pv.cnt = L;
+  pa.coeffs = m.size == 1 ? (Fr *)d_ca.ensure(sizeof(Fr) * N) : nullptr;
+  pv.coeffs = m.size == 1 ? (Fr *)d_cv.ensure(sizeof(Fr) * N) : nullptr;
+  Fr *YA = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * L), *YV = (Fr *)c->prove_ws[9].ensure(sizeof(Fr) * L);
+  TNS_HIP(hipMemcpyAsync(YA, A, sizeof(Fr) * L, hipMemcpyDeviceToDevice, st));
+  TNS_HIP(hipMemcpyAsync(YV, V, sizeof(Fr) * L, hipMemcpyDeviceToDevice, st));
   pa.y = YA;
   pv.y = YV;
   tm[1] = t_int.ms();
   Timer t_com;
-  G1Affine Ca = commit_evals(c, srs->s, pa);
-  G1Affine Cv = commit_evals(c, srs->s, pv);
+  G1Affine Ca = commit_evals(c, srs->s, pa, m);
+  G1Affine Cv = commit_evals(c, srs->s, pv, m);
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
   tm[2] = t_com.ms();
@@ -626,7 +724,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tr.append_fr(commitment_hash(Cv));
   // ---- sum-check over the addr / value / op-type MLEs + openings (src/twist.rs:177-243)
   Fr *mles[3] = {A, V, O};
-  fill_common_tail(c, srs->s, tr, mles, 3, nv, pa, pv, out, tm, d_s);
+  fill_common_tail(c, srs->s, tr, mles, 3, nv, pa, pv, out, tm, d_s, m);
   TNS_HIP(hipStreamSynchronize(st));
   tm[5] = total.ms();
 }
@@ -634,7 +732,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
 int tns_twist_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *addr,
                     const uint64_t *value, const uint8_t *is_write, size_t n_ops, tns_proof *out) {
   return guarded([&]() {
-    twist_core(ctx, srs, params, addr, value, is_write, n_ops, out, hipMemcpyHostToDevice);
+    twist_core(ctx, srs, params, comm_self(), addr, value, is_write, n_ops, n_ops, out, hipMemcpyHostToDevice);
     return TNS_OK;
   });
 }
@@ -642,68 +740,95 @@ int tns_twist_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, 
 int tns_twist_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *d_addr,
                            const uint64_t *d_value, const uint8_t *d_is_write, size_t n_ops, tns_proof *out) {
   return guarded([&]() {
-    twist_core(ctx, srs, params, d_addr, d_value, d_is_write, n_ops, out, hipMemcpyDeviceToDevice);
+    twist_core(ctx, srs, params, comm_self(), d_addr, d_value, d_is_write, n_ops, n_ops, out,
+               hipMemcpyDeviceToDevice);
     return TNS_OK;
   });
 }
 
-// Shout::prove (src/shout.rs:97-222)
-static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *entries,
-                       size_t n_entries, const uint64_t *indices, size_t n_lookups, tns_proof *out,
-                       hipMemcpyKind kind) {
+int tns_twist_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, tns_comm *comm,
+                            const uint64_t *d_addr, const uint64_t *d_value, const uint8_t *d_is_write,
+                            size_t n_local, uint64_t n_total, tns_proof *out) {
+  return guarded([&]() {
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    twist_core(ctx, srs, params, *comm->c, d_addr, d_value, d_is_write, n_local, n_total, out,
+               hipMemcpyDeviceToDevice);
+    return TNS_OK;
+  });
+}
+
+// Shout::prove (src/shout.rs:97-222) for this rank's slices of the table (T) and the lookup
+// index vector (M), sliced like twist_core's trace.
+static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, Comm &m, const uint64_t *entries,
+                       size_t n_entries, uint64_t n_entries_total, const uint64_t *indices, size_t n_lookups,
+                       uint64_t n_lookups_total, tns_proof *out, hipMemcpyKind kind) {
   Timer total;
   CtxScope g(&ctx->c);
   Ctx *c = &ctx->c;
   hipStream_t st = c->stream;
   std::memset(out, 0, sizeof *out);
-  if (n_lookups > params->max_operations)  // src/shout.rs:98-102
+  if (n_lookups_total > params->max_operations)  // src/shout.rs:98-102
     throw Error(TNS_ERR_INVALID_PARAMETERS, "Too many lookup operations");
-  const size_t T = next_pow2(n_entries), M = next_pow2(n_lookups);  // :105, :116
+  const size_t T = next_pow2(n_entries_total), M = next_pow2(n_lookups_total);  // :105, :116
   const unsigned nv = ilog2_exact(M);
   if (nv > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many lookups");
+  check_shard(m, T, "table");
+  check_shard(m, M, "lookup");
+  const size_t LT = T / m.size, LM = M / m.size, firstT = (size_t)m.rank * LT, firstM = (size_t)m.rank * LM;
+  if (n_entries != slice_count(n_entries_total, firstT, LT) || n_lookups != slice_count(n_lookups_total, firstM, LM))
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "local table / lookup count does not match this rank's slice");
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
   Timer t_h2d;
   DevBuf &d_idx_raw = c->prove_ws[0], &d_bad = c->prove_ws[1], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3],
          &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
-  Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * T), *I = (Fr *)d_i.ensure(sizeof(Fr) * M);
-  fr_fill_zero_dev(c, TB, T);
-  fr_fill_zero_dev(c, I, M);
+  Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * LT), *I = (Fr *)d_i.ensure(sizeof(Fr) * LM);
+  fr_fill_zero_dev(c, TB, LT);
+  fr_fill_zero_dev(c, I, LM);
   if (n_entries) TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
+  // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
+  unsigned hbad = 0;
+  const uint64_t *ir = indices;
   if (n_lookups) {
-    const uint64_t *ir = indices;
     if (kind == hipMemcpyHostToDevice) {
       uint64_t *dir = (uint64_t *)d_idx_raw.ensure(8 * n_lookups);
       TNS_HIP(hipMemcpyAsync(dir, indices, 8 * n_lookups, hipMemcpyHostToDevice, st));
       ir = dir;
     }
-    // LookupTable::lookup bounds (src/shout.rs:44-50)
     unsigned *bad = (unsigned *)d_bad.ensure(sizeof(unsigned));
     TNS_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
-    k_max_index_check<<<grid_for(n_lookups, 256), 256, 0, st>>>(ir, n_lookups, n_entries, bad);
+    k_max_index_check<<<grid_for(n_lookups, 256), 256, 0, st>>>(ir, n_lookups, n_entries_total, bad);
     TNS_LAUNCH_CHECK();
-    unsigned hbad = 0;
     TNS_HIP(hipMemcpyAsync(&hbad, bad, sizeof hbad, hipMemcpyDeviceToHost, st));
     TNS_HIP(hipStreamSynchronize(st));
-    if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
-    to_mont_u64_dev(c, ir, I, n_lookups);
   }
+  if (m.size > 1) {
+    std::vector<unsigned> flags(m.size);
+    m.allgather(c, &hbad, sizeof hbad, flags.data());
+    for (unsigned f : flags) hbad |= f;
+  }
+  if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
+  if (n_lookups) to_mont_u64_dev(c, ir, I, n_lookups);
   TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   Timer t_int;
   EvalPoly pt, pi;
   pt.N = T;
   pi.N = M;
-  pt.coeffs = (Fr *)d_ct.ensure(sizeof(Fr) * T);
-  pi.coeffs = (Fr *)d_ci.ensure(sizeof(Fr) * M);
-  Fr *YI = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * M);  // the sum-check folds I in place
-  TNS_HIP(hipMemcpyAsync(YI, I, sizeof(Fr) * M, hipMemcpyDeviceToDevice, st));
+  pt.first = firstT;
+  pi.first = firstM;
+  pt.cnt = LT;
+  pi.cnt = LM;
+  pt.coeffs = m.size == 1 ? (Fr *)d_ct.ensure(sizeof(Fr) * T) : nullptr;
+  pi.coeffs = m.size == 1 ? (Fr *)d_ci.ensure(sizeof(Fr) * M) : nullptr;
+  Fr *YI = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * LM);  // the sum-check folds I in place
+  TNS_HIP(hipMemcpyAsync(YI, I, sizeof(Fr) * LM, hipMemcpyDeviceToDevice, st));
   pt.y = TB;
   pi.y = YI;
   tm[1] = t_int.ms();
   Timer t_com;
-  G1Affine Ct = commit_evals(c, srs->s, pt);  // table first (src/shout.rs:125-133)
-  G1Affine Ci = commit_evals(c, srs->s, pi);
+  G1Affine Ct = commit_evals(c, srs->s, pt, m);  // table first (src/shout.rs:125-133)
+  G1Affine Ci = commit_evals(c, srs->s, pi, m);
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);
   tm[2] = t_com.ms();
@@ -713,7 +838,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tr.append_label("index_commitment");
   tr.append_fr(commitment_hash(Ci));
   Fr *mles[1] = {I};  // the closure evaluates only the index MLE (src/shout.rs:175)
-  fill_common_tail(c, srs->s, tr, mles, 1, nv, pt, pi, out, tm, d_s);
+  fill_common_tail(c, srs->s, tr, mles, 1, nv, pt, pi, out, tm, d_s, m);
   TNS_HIP(hipStreamSynchronize(st));
   tm[5] = total.ms();
 }
@@ -721,7 +846,8 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
 int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *entries,
                     size_t n_entries, const uint64_t *indices, size_t n_lookups, tns_proof *out) {
   return guarded([&]() {
-    shout_core(ctx, srs, params, entries, n_entries, indices, n_lookups, out, hipMemcpyHostToDevice);
+    shout_core(ctx, srs, params, comm_self(), entries, n_entries, n_entries, indices, n_lookups, n_lookups, out,
+               hipMemcpyHostToDevice);
     return TNS_OK;
   });
 }
@@ -729,10 +855,62 @@ int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, 
 int tns_shout_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, const uint64_t *d_entries,
                            size_t n_entries, const uint64_t *d_indices, size_t n_lookups, tns_proof *out) {
   return guarded([&]() {
-    shout_core(ctx, srs, params, d_entries, n_entries, d_indices, n_lookups, out, hipMemcpyDeviceToDevice);
+    shout_core(ctx, srs, params, comm_self(), d_entries, n_entries, n_entries, d_indices, n_lookups, n_lookups,
+               out, hipMemcpyDeviceToDevice);
     return TNS_OK;
   });
 }
+
+int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *params, tns_comm *comm,
+                            const uint64_t *d_entries, size_t n_entries_local, uint64_t n_entries_total,
+                            const uint64_t *d_indices, size_t n_lookups_local, uint64_t n_lookups_total,
+                            tns_proof *out) {
+  return guarded([&]() {
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    shout_core(ctx, srs, params, *comm->c, d_entries, n_entries_local, n_entries_total, d_indices, n_lookups_local,
+               n_lookups_total, out, hipMemcpyDeviceToDevice);
+    return TNS_OK;
+  });
+}
+
+// ---------------------------------------------------------------- communicators
+int tns_comm_unique_id(uint8_t uid[128]) {
+  return guarded([&]() {
+    comm_unique_id(uid);
+    return TNS_OK;
+  });
+}
+
+int tns_comm_create(tns_ctx *ctx, int rank, int size, const uint8_t uid[128], tns_comm **out) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    tns_comm *cm = new tns_comm();
+    try {
+      cm->c = comm_rccl_new(&ctx->c, rank, size, uid);
+    } catch (...) {
+      delete cm;
+      throw;
+    }
+    *out = cm;
+    return TNS_OK;
+  });
+}
+
+int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user, tns_comm **out) {
+  return guarded([&]() {
+    tns_comm *cm = new tns_comm();
+    try {
+      cm->c = comm_callback_new(rank, size, fn, user);
+    } catch (...) {
+      delete cm;
+      throw;
+    }
+    *out = cm;
+    return TNS_OK;
+  });
+}
+
+void tns_comm_destroy(tns_comm *comm) { delete comm; }
 
 // ---------------------------------------------------------------- device buffers
 int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer **out) {
@@ -824,25 +1002,44 @@ void tns_fq_to_canonical(const uint64_t *in, size_t n, uint64_t *out) {
   });
 }
 
+// ProtocolBenchmarks trace (src/benchmarks.rs:88-99), operations [first, first + count) of
+// an n_total-operation run (the memory state is replayed from operation 0)
+static void bench_trace_core(size_t memory_size, uint64_t n_total, uint64_t first, size_t count, uint64_t *addr,
+                             uint64_t *value, uint8_t *is_write) {
+  if (memory_size == 0 || (memory_size & (memory_size - 1)))
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "Memory size must be power of 2");
+  if (first + count > n_total) throw Error(TNS_ERR_INVALID_PARAMETERS, "slice beyond the trace");
+  std::vector<uint64_t> mem(memory_size, 0);
+  for (uint64_t i = 0; i < first + count; i++) {
+    const bool out = i >= first;
+    if (i % 3 == 0) {
+      const size_t a = i % memory_size;
+      mem[a] = i * 42;
+      if (out) {
+        addr[i - first] = a;
+        value[i - first] = mem[a];
+        is_write[i - first] = 1;
+      }
+    } else if (out) {
+      const size_t a = (i / 2) % memory_size;
+      addr[i - first] = a;
+      value[i - first] = mem[a];
+      is_write[i - first] = 0;
+    }
+  }
+}
+
 int tns_bench_trace(size_t memory_size, size_t n_ops, uint64_t *addr, uint64_t *value, uint8_t *is_write) {
   return guarded([&]() {
-    if (memory_size == 0 || (memory_size & (memory_size - 1)))
-      throw Error(TNS_ERR_INVALID_PARAMETERS, "Memory size must be power of 2");
-    std::vector<uint64_t> mem(memory_size, 0);
-    for (size_t i = 0; i < n_ops; i++) {
-      if (i % 3 == 0) {
-        size_t a = i % memory_size;
-        mem[a] = (uint64_t)i * 42;
-        addr[i] = a;
-        value[i] = mem[a];
-        is_write[i] = 1;
-      } else {
-        size_t a = (i / 2) % memory_size;
-        addr[i] = a;
-        value[i] = mem[a];
-        is_write[i] = 0;
-      }
-    }
+    bench_trace_core(memory_size, n_ops, 0, n_ops, addr, value, is_write);
+    return TNS_OK;
+  });
+}
+
+int tns_bench_trace_slice(size_t memory_size, uint64_t n_total, uint64_t first, size_t count, uint64_t *addr,
+                          uint64_t *value, uint8_t *is_write) {
+  return guarded([&]() {
+    bench_trace_core(memory_size, n_total, first, count, addr, value, is_write);
     return TNS_OK;
   });
 }

@@ -1,0 +1,117 @@
+// comm.cpp -- the exchange steps of one proof sharded across ranks (one process per GPU).
+//
+// A sharded Twist/Shout proof exchanges only a few hundred bytes per step:
+// partial G1 sums of the commitment / opening MSMs, the barycentric partial sum and node
+// product of each opening, and one folded value per MLE table after the local sum-check
+// rounds.  RCCL has no elliptic-curve or mod-r reduction, so every exchange is an
+// allgather of the partials followed by the same (order-independent) combination on every
+// rank -- all ranks then hold identical transcripts and proofs.
+//
+// Transports: RCCL (ncclAllGather over xGMI on the context stream, staged through a small
+// device buffer), a host callback (any launcher's collective, e.g. torch.distributed), or
+// the trivial one-rank communicator used by the unsharded entry points.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace tns {
+
+namespace {
+
+struct SelfComm final : Comm {
+  void allgather(Ctx *, const void *send, size_t bytes, void *recv) override { std::memcpy(recv, send, bytes); }
+};
+
+struct CallbackComm final : Comm {
+  tns_allgather_fn fn;
+  void *user;
+  void allgather(Ctx *, const void *send, size_t bytes, void *recv) override {
+    const int st = fn(user, send, bytes, recv);
+    if (st != 0) throw Error(TNS_ERR_DEVICE, "allgather callback failed with status " + std::to_string(st));
+  }
+};
+
+#define TNS_NCCL(call)                                                                          \
+  do {                                                                                          \
+    ncclResult_t _r = (call);                                                                   \
+    if (_r != ncclSuccess) throw Error(TNS_ERR_DEVICE, std::string("RCCL: ") + ncclGetErrorString(_r)); \
+  } while (0)
+
+struct RcclComm final : Comm {
+  ncclComm_t comm = nullptr;
+  DevBuf send_b, recv_b;
+  ~RcclComm() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  void allgather(Ctx *c, const void *send, size_t bytes, void *recv) override {
+    void *ds = send_b.ensure(bytes ? bytes : 1), *dr = recv_b.ensure(bytes * size ? bytes * size : 1);
+    TNS_HIP(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, c->stream));
+    TNS_NCCL(ncclAllGather(ds, dr, bytes, ncclUint8, comm, c->stream));
+    TNS_HIP(hipMemcpyAsync(recv, dr, bytes * size, hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipStreamSynchronize(c->stream));
+  }
+};
+
+}  // namespace
+
+Comm &comm_self() {
+  static SelfComm self;
+  return self;
+}
+
+Comm *comm_callback_new(int rank, int size, tns_allgather_fn fn, void *user) {
+  if (size < 1 || rank < 0 || rank >= size || !fn) throw Error(TNS_ERR_INVALID_PARAMETERS, "bad communicator shape");
+  CallbackComm *c = new CallbackComm();
+  c->rank = rank;
+  c->size = size;
+  c->fn = fn;
+  c->user = user;
+  return c;
+}
+
+void comm_unique_id(uint8_t out[128]) {
+  static_assert(sizeof(ncclUniqueId) <= 128, "ncclUniqueId larger than the ABI's 128 bytes");
+  ncclUniqueId id;
+  TNS_NCCL(ncclGetUniqueId(&id));
+  std::memset(out, 0, 128);
+  std::memcpy(out, &id, sizeof id);
+}
+
+Comm *comm_rccl_new(Ctx *c, int rank, int size, const uint8_t uid[128]) {
+  if (size < 1 || rank < 0 || rank >= size) throw Error(TNS_ERR_INVALID_PARAMETERS, "bad communicator shape");
+  RcclComm *r = new RcclComm();
+  r->rank = rank;
+  r->size = size;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof id);
+  TNS_HIP(hipSetDevice(c->device));
+  ncclResult_t st = ncclCommInitRank(&r->comm, size, id, rank);
+  if (st != ncclSuccess) {
+    delete r;
+    throw Error(TNS_ERR_DEVICE, std::string("RCCL init: ") + ncclGetErrorString(st));
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- combined exchanges
+G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part) {
+  if (m.size == 1) return part;
+  std::vector<G1Xyzz> all(m.size);
+  m.allgather(c, &part, sizeof part, all.data());
+  G1Xyzz acc = G1Xyzz::inf();
+  for (const auto &p : all) acc = xyzz_add(acc, p);
+  return acc;
+}
+
+std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k) {
+  std::vector<Fr> all(k * m.size);
+  m.allgather(c, part, sizeof(Fr) * k, all.data());
+  return all;
+}
+
+}  // namespace tns

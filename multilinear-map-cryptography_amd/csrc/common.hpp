@@ -10,6 +10,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/tns.h"
@@ -100,7 +101,9 @@ struct Srs {
   // also yields the Lagrange basis of the nodes {0..N-1}: G * L_j(tau) (lagrange.hip).
   bool has_tau = false;
   Fr tau;
-  mutable std::map<unsigned, LagrangeBasis *> lagrange;  // log N -> basis (cache)
+  // (log N, first node, node count) -> basis slice (cache)
+  mutable std::map<std::tuple<unsigned, size_t, size_t>, LagrangeBasis *> lagrange;
+  size_t first = 0, held = 0;  // points[0..held) are g1_powers[first .. first + held) (sharded SRS)
   mutable FixedBase *fb = nullptr;                        // window table of `points` (lazy)
   Srs() = default;
   Srs(const Srs &) = delete;
@@ -180,7 +183,7 @@ struct Ctx {
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
   std::map<uint32_t, DevBuf *> pass_tw;  // four-step pass twiddles keyed by (lo << 8 | r)
-  std::map<unsigned, DevBuf *> bary_w;   // log N -> barycentric weights of nodes {0..N-1}
+  std::map<std::tuple<unsigned, size_t, size_t>, DevBuf *> bary_w;  // (log N, first, count) -> weights
   bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
   bool msm_tables = true;                // shared-bucket MSM on fixed bases with window tables
   KernelProfiler prof;
@@ -237,7 +240,8 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
 // poly.hip
 // q[i] = c[i+1] + z q[i+1] (synthetic division by x - z); returns P(z).  q may be null.
 Fr synthetic_division_dev(Ctx *c, const Fr *coeffs, size_t n, const Fr &z, Fr *q);
-void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out);
+// g1_powers[first .. first + n) = G * tau^i
+void srs_generate_dev(Ctx *c, const Fr &tau, size_t first, size_t n, G1Affine *out);
 void to_mont_u64_dev(Ctx *c, const uint64_t *in, Fr *out, size_t n);
 void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 
@@ -255,13 +259,31 @@ void factorial_tables_dev(Ctx *c, size_t nf, Fr *fact, Fr *ifact);
 void fixed_base_mul_dev(Ctx *c, const Fr *scalars_canon, size_t n, G1Affine *out);
 void xyzz_to_affine_batch_dev(Ctx *c, const G1Xyzz *in, size_t n, G1Affine *out, Fq *prefix_scratch);
 
-// lagrange.hip: KZG on evaluations over the nodes {0..N-1}
-// Lagrange basis G * L_j(tau) for N (cached in srs); nullptr when srs has no tau or
-// tau is itself a node.
-const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N);
-// v = P(z) and q(j) = (P(j) - v) / (j - z) on the nodes (q: device, N), for z not a
-// node; returns false (nothing written) when z is a node.
-bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q);
+// lagrange.hip: KZG on evaluations over the nodes {0..N-1}, for the node slice
+// [first, first + cnt) a rank holds (first = 0, cnt = N unsharded).
+// Basis slice G * L_j(tau) (cached in srs); nullptr when srs has no tau or tau is a node.
+const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t first, size_t cnt);
+// inv[i] = 1 / (z - j) (j = first + i); ell_part = prod (z - j); sum_part = sum w_j y_j / (z - j)
+// over the slice.  P(z) = (prod of all ell parts) * (sum of all sum parts).  z not a node.
+void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size_t cnt, const Fr &z, Fr *inv,
+                               Fr *ell_part, Fr *sum_part);
+// q_i = (v - y_i) * inv_i in place: the quotient's values on the slice
+void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
+bool fr_is_node(const Fr &x, size_t N);
+
+// comm.cpp: the exchange steps of a sharded proof
+struct Comm {
+  int rank = 0, size = 1;
+  virtual ~Comm() = default;
+  // every rank's `bytes` from `send`, in rank order, into recv (size * bytes)
+  virtual void allgather(Ctx *c, const void *send, size_t bytes, void *recv) = 0;
+};
+Comm &comm_self();
+Comm *comm_callback_new(int rank, int size, tns_allgather_fn fn, void *user);
+Comm *comm_rccl_new(Ctx *c, int rank, int size, const uint8_t uid[128]);
+void comm_unique_id(uint8_t out[128]);
+G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part);
+std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k);
 
 // host-side helpers (transcript.cpp)
 struct HostTranscript {

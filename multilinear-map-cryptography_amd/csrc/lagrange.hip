@@ -23,6 +23,7 @@
 // product of the chain products.
 #include <hip/hip_runtime.h>
 
+#include <tuple>
 #include <vector>
 
 #include "common.hpp"
@@ -58,21 +59,6 @@ __global__ void __launch_bounds__(1024) k_prod_reduce(const Fr *__restrict__ in,
     __syncthreads();
   }
   if (threadIdx.x == 0) out[0] = lds[0];
-}
-
-// out[0] = scale[0] * sum_i in[i] (one block)
-__global__ void __launch_bounds__(1024) k_sum_reduce_scaled(const Fr *__restrict__ in, size_t n,
-                                                            const Fr *__restrict__ scale, Fr *__restrict__ out) {
-  __shared__ Fr lds[1024];
-  Fr acc = Fr::zero();
-  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = add(acc, in[i]);
-  lds[threadIdx.x] = acc;
-  __syncthreads();
-  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) lds[threadIdx.x] = add(lds[threadIdx.x], lds[threadIdx.x + s]);
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[0] = mul(lds[0], scale[0]);
 }
 
 // Backward sweep of chain t: inv_i = 1/(x - i) from pre[i] and the chain inverse.
@@ -113,39 +99,66 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
 }
 
 // q_i = (v - y_i) * inv_i, in place over inv
-__global__ void __launch_bounds__(256) k_node_quotient(const Fr *__restrict__ y, const Fr *__restrict__ v,
-                                                       size_t n, Fr *__restrict__ q) {
-  const Fr vv = v[0];
+__global__ void __launch_bounds__(256) k_node_quotient(const Fr *__restrict__ y, Fr v, size_t n, Fr *__restrict__ q) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
-    q[i] = mul(sub(vv, y[i]), q[i]);
+    q[i] = mul(sub(v, y[i]), q[i]);
 }
 
-// w_j = (-1)^(N-1-j) / (j! (N-1-j)!)
-__global__ void __launch_bounds__(256) k_bary_weights(const Fr *__restrict__ ifact, size_t n, Fr *__restrict__ w) {
-  for (size_t j = blockIdx.x * (size_t)blockDim.x + threadIdx.x; j < n; j += (size_t)gridDim.x * blockDim.x) {
-    Fr x = mul(ifact[j], ifact[n - 1 - j]);
-    w[j] = ((n - 1 - j) & 1) ? neg(x) : x;
+// w[i] = w_j for j = first + i:  w_j = (-1)^(N-1-j) / (j! (N-1-j)!)
+__global__ void __launch_bounds__(256) k_bary_weights(const Fr *__restrict__ ifact, size_t N, size_t first,
+                                                      size_t cnt, Fr *__restrict__ w) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < cnt; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t j = first + i;
+    Fr x = mul(ifact[j], ifact[N - 1 - j]);
+    w[i] = ((N - 1 - j) & 1) ? neg(x) : x;
   }
 }
 
-static const Fr *bary_weights(Ctx *c, size_t N) {
-  const unsigned lg = ilog2_exact(N);
-  auto it = c->bary_w.find(lg);
+// cp[t] = prod over the chain t of (x - i), i = t, t + T, ... < n (no per-node output)
+__global__ void __launch_bounds__(256) k_node_prod(Fr x, size_t n, size_t T, Fr Tm, Fr *__restrict__ cp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)t));
+  Fr acc = Fr::one();
+  for (size_t i = t; i < n; i += T) {
+    acc = mul(acc, d);
+    d = sub(d, Tm);
+  }
+  cp[t] = acc;
+}
+
+// out[0] = sum_i in[i] (one block)
+__global__ void __launch_bounds__(1024) k_sum_reduce(const Fr *__restrict__ in, size_t n, Fr *__restrict__ out) {
+  __shared__ Fr lds[1024];
+  Fr acc = Fr::zero();
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = add(acc, in[i]);
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) lds[threadIdx.x] = add(lds[threadIdx.x], lds[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = lds[0];
+}
+
+// barycentric weights of the nodes [first, first + cnt) of {0..N-1} (cached per slice)
+static const Fr *bary_weights(Ctx *c, size_t N, size_t first, size_t cnt) {
+  const auto key = std::make_tuple(ilog2_exact(N), first, cnt);
+  auto it = c->bary_w.find(key);
   if (it != c->bary_w.end()) return it->second->as<Fr>();
   DevBuf fact, ifact;
   Fr *f = (Fr *)fact.ensure(sizeof(Fr) * N), *fi = (Fr *)ifact.ensure(sizeof(Fr) * N);
   factorial_tables_dev(c, N, f, fi);
   DevBuf *b = new DevBuf();
-  Fr *w = (Fr *)b->ensure(sizeof(Fr) * N);
-  k_bary_weights<<<grid_for(N, 256), 256, 0, c->stream>>>(fi, N, w);
+  Fr *w = (Fr *)b->ensure(sizeof(Fr) * cnt);
+  k_bary_weights<<<grid_for(cnt, 256), 256, 0, c->stream>>>(fi, N, first, cnt, w);
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipStreamSynchronize(c->stream));  // fact/ifact die here
-  c->bary_w[lg] = b;
+  c->bary_w[key] = b;
   return w;
 }
 
-// x (Montgomery) equals one of the nodes 0..N-1?
-static bool is_node(const Fr &x, size_t N) {
+bool fr_is_node(const Fr &x, size_t N) {
   Fr k = from_mont(x);
   for (int i = 2; i < 8; i++)
     if (k.v[i]) return false;
@@ -153,68 +166,91 @@ static bool is_node(const Fr &x, size_t N) {
   return v < N;
 }
 
+static size_t chain_count(size_t n) { return n < NODE_THREADS ? n : NODE_THREADS; }
+
 struct NodeSweep {
   size_t T;
   Fr Tm;
-  Fr *cp, *sp, *dev;  // chain products, partial sums, device scalars (ell, v)
+  Fr *cp, *sp, *dev;  // chain products, partial sums, device scalars
 };
 
-static NodeSweep node_sweep_begin(Ctx *c, const Fr &x, size_t N, Fr *pre) {
+// chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
+static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre) {
   NodeSweep s;
-  s.T = N < NODE_THREADS ? N : NODE_THREADS;
+  s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
   Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (2 * s.T + 4));
   s.cp = ws;
   s.sp = ws + s.T;
   s.dev = ws + 2 * s.T;
-  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(x, N, s.T, s.Tm, pre, s.cp);
+  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, pre, s.cp);
   TNS_LAUNCH_CHECK();
-  k_prod_reduce<<<1, 1024, 0, c->stream>>>(s.cp, s.T, s.dev);  // ell(x)
+  k_prod_reduce<<<1, 1024, 0, c->stream>>>(s.cp, s.T, s.dev);
   TNS_LAUNCH_CHECK();
   return s;
 }
 
-const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N) {
+static Fr fr_shift(const Fr &x, size_t first) { return sub(x, from_u64<FrCfg>((uint64_t)first)); }
+
+const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t first, size_t cnt) {
   if (!c->lagrange_commit || !srs.has_tau || N == 0 || (N & (N - 1))) return nullptr;
-  if (is_node(srs.tau, N)) return nullptr;
-  const unsigned lg = ilog2_exact(N);
-  auto it = srs.lagrange.find(lg);
+  if (first + cnt > N || cnt == 0) throw Error(TNS_ERR_INVALID_PARAMETERS, "node slice outside 0..N-1");
+  if (fr_is_node(srs.tau, N)) return nullptr;
+  const auto key = std::make_tuple(ilog2_exact(N), first, cnt);
+  auto it = srs.lagrange.find(key);
   if (it != srs.lagrange.end()) return it->second;
-  const Fr *w = bary_weights(c, N);
+  const Fr *w = bary_weights(c, N, first, cnt);
+  // ell(tau) over all N nodes
+  DevBuf ellb;
+  const size_t TG = chain_count(N);
+  Fr *ecp = (Fr *)ellb.ensure(sizeof(Fr) * (TG + 1));
+  k_node_prod<<<grid_for(TG, 256, 1u << 30), 256, 0, c->stream>>>(srs.tau, N, TG, from_u64<FrCfg>((uint64_t)TG),
+                                                                   ecp);
+  TNS_LAUNCH_CHECK();
+  k_prod_reduce<<<1, 1024, 0, c->stream>>>(ecp, TG, ecp + TG);
+  TNS_LAUNCH_CHECK();
   DevBuf scal;
-  Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * N);  // pre, then canonical L_j(tau) in place
-  NodeSweep s = node_sweep_begin(c, srs.tau, N, sc);
-  k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(srs.tau, N, s.T, s.Tm, sc, s.cp, w,
-                                                                           nullptr, s.dev, sc, nullptr);
+  Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * cnt);  // pre, then canonical L_j(tau) in place
+  const Fr xs = fr_shift(srs.tau, first);
+  NodeSweep s = node_sweep_begin(c, xs, cnt, sc);
+  k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, sc, s.cp, w, nullptr,
+                                                                           ecp + TG, sc, nullptr);
   TNS_LAUNCH_CHECK();
   LagrangeBasis *b = new LagrangeBasis();
   try {
-    G1Affine *pts = (G1Affine *)b->points.ensure(sizeof(G1Affine) * N);
-    fixed_base_mul_dev(c, sc, N, pts);  // synchronises
-    if (N >= ((size_t)1 << 12)) b->fb = fixed_base_build_dev(c, pts, N);
+    G1Affine *pts = (G1Affine *)b->points.ensure(sizeof(G1Affine) * cnt);
+    fixed_base_mul_dev(c, sc, cnt, pts);  // synchronises
+    if (cnt >= ((size_t)1 << 12)) b->fb = fixed_base_build_dev(c, pts, cnt);
   } catch (...) {
     delete b;
     throw;
   }
-  srs.lagrange[lg] = b;
+  srs.lagrange[key] = b;
   return b;
 }
 
-bool lagrange_quotient_dev(Ctx *c, const Fr *y, size_t N, const Fr &z, Fr *value, Fr *q) {
-  if (N == 0 || is_node(z, N)) return false;
-  TNS_PROF(c, "open_scan", 32.0 * 6 * N);  // q: pre write/read, inv write/read, y twice
-  const Fr *w = bary_weights(c, N);
-  NodeSweep s = node_sweep_begin(c, z, N, q);
-  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(z, N, s.T, s.Tm, q, s.cp, w, y,
-                                                                            nullptr, q, s.sp);
+void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size_t cnt, const Fr &z, Fr *inv,
+                               Fr *ell_part, Fr *sum_part) {
+  TNS_PROF(c, "open_scan", 32.0 * 4 * cnt);  // pre write/read, inv write, y, w
+  const Fr *w = bary_weights(c, N, first, cnt);
+  const Fr xs = fr_shift(z, first);
+  NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.cp, w, y,
+                                                                            nullptr, inv, s.sp);
   TNS_LAUNCH_CHECK();
-  k_sum_reduce_scaled<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev, s.dev + 1);  // v = ell(z) * sum
+  k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
   TNS_LAUNCH_CHECK();
-  k_node_quotient<<<grid_for(N, 256), 256, 0, c->stream>>>(y, s.dev + 1, N, q);
-  TNS_LAUNCH_CHECK();
-  TNS_HIP(hipMemcpyAsync(value, s.dev + 1, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  Fr h[2];
+  TNS_HIP(hipMemcpyAsync(h, s.dev, sizeof h, hipMemcpyDeviceToHost, c->stream));
   TNS_HIP(hipStreamSynchronize(c->stream));
-  return true;
+  *ell_part = h[0];
+  *sum_part = h[1];
+}
+
+void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q) {
+  TNS_PROF(c, "open_scan", 32.0 * 3 * cnt);
+  k_node_quotient<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y, v, cnt, q);
+  TNS_LAUNCH_CHECK();
 }
 
 }  // namespace tns

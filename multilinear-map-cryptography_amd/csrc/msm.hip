@@ -421,7 +421,8 @@ FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n) {
 
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n) {
   if (n < ((size_t)1 << 16) || !c->msm_tables) return nullptr;
-  if (!srs.fb) srs.fb = fixed_base_build_dev(c, srs.points.as<G1Affine>(), srs.n);
+  if (srs.first != 0 || srs.held < n) return nullptr;
+  if (!srs.fb) srs.fb = fixed_base_build_dev(c, srs.points.as<G1Affine>(), srs.held);
   return srs.fb;
 }
 

@@ -256,10 +256,10 @@ static void fixed_base_slabs(Ctx *c, size_t n, G1Affine *out, Fill fill) {
   TNS_HIP(hipStreamSynchronize(c->stream));
 }
 
-void srs_generate_dev(Ctx *c, const Fr &tau, size_t n, G1Affine *out) {
+void srs_generate_dev(Ctx *c, const Fr &tau, size_t first, size_t n, G1Affine *out) {
   fixed_base_slabs(c, n, out, [&](size_t off, size_t m, Fr *pw) -> const Fr * {
     size_t chunks = (m + SRS_POW_CHUNK - 1) / SRS_POW_CHUNK;
-    k_tau_powers<<<grid_for(chunks, 256, 1u << 30), 256, 0, c->stream>>>(tau, off, m, pw);
+    k_tau_powers<<<grid_for(chunks, 256, 1u << 30), 256, 0, c->stream>>>(tau, first + off, m, pw);
     TNS_LAUNCH_CHECK();
     return pw;
   });

@@ -634,6 +634,17 @@ class Twist:
     def prove(self, trace: MemoryTrace) -> TwistProof:
         return self.prove_soa(*trace.soa())
 
+    def prove_sharded(self, comm: "Comm", addr: np.ndarray, value: np.ndarray, is_write: np.ndarray,
+                      n_total: int) -> TwistProof:
+        """This rank's slice (shard_slice(n_total, rank, size)) of one trace; every rank
+        returns the same proof as the unsharded prove."""
+        ctx = self.prover_params.commitment_params.srs.ctx
+        n = len(addr)
+        da = _nonempty_buf(ctx, addr, np.uint64)
+        dv = _nonempty_buf(ctx, np.asarray(value, dtype=np.uint64).reshape(-1, 4), np.uint64, 4)
+        dw = _nonempty_buf(ctx, is_write, np.uint8)
+        return twist_proof_from_raw(twist_prove_sharded_resident(self.prover_params, comm, da, dv, dw, n, n_total))
+
 
 # ----------------------------------------------------------------------------- Shout
 @dataclass(frozen=True)
@@ -691,6 +702,16 @@ class Shout:
         u = _unpack_proof(pr, 1)
         return ShoutProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"], u["z"], u["chals"])
 
+    def prove_sharded(self, comm: "Comm", entries_mont: np.ndarray, n_entries_total: int, indices: np.ndarray,
+                      n_lookups_total: int) -> ShoutProof:
+        """This rank's slices of the table and of the lookup indices (shard_slice)."""
+        ctx = self.prover_params.commitment_params.srs.ctx
+        e = np.asarray(entries_mont, dtype=np.uint64).reshape(-1, 4)
+        de = _nonempty_buf(ctx, e, np.uint64, 4)
+        di = _nonempty_buf(ctx, indices, np.uint64)
+        return shout_proof_from_raw(shout_prove_sharded_resident(self.prover_params, comm, de, len(e),
+                                                                 n_entries_total, di, len(indices), n_lookups_total))
+
     def prove(self, table: LookupTable) -> ShoutProof:
         e = to_mont(table.entries) if table.entries else np.zeros((0, 4), dtype=np.uint64)
         ix = np.array([l.index for l in table.lookups], dtype=np.uint64)
@@ -741,6 +762,142 @@ def msm_resident(params: CommitmentParams, scalars: DeviceBuffer, n: int) -> np.
     return out
 
 
+# ----------------------------------------------------------------------------- one proof across GPUs
+_AllgatherFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+
+class Comm:
+    """Communicator of one sharded proof (tns_comm): the allgathers of partial MSM sums,
+    barycentric partials and folded table values."""
+
+    def __init__(self, handle: C.c_void_p, rank: int, size: int, keep=None):
+        self.handle, self.rank, self.size, self._keep = handle, rank, size, keep
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(N.load().tns_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, ctx: Context, rank: int, size: int, uid: bytes) -> "Comm":
+        """RCCL communicator (ncclAllGather over xGMI); uid from Comm.unique_id() on rank 0."""
+        h = C.c_void_p()
+        _check(N.load().tns_comm_create(ctx.handle, rank, size, (C.c_uint8 * 128)(*uid), C.byref(h)))
+        return cls(h, rank, size)
+
+    @classmethod
+    def from_allgather(cls, rank: int, size: int, fn) -> "Comm":
+        """fn(local: bytes) -> bytes: every rank's bytes concatenated in rank order."""
+        def cb(user, send, nbytes, recv):
+            try:
+                out = fn(C.string_at(send, nbytes))
+                if len(out) != nbytes * size:
+                    return 2
+                C.memmove(recv, out, len(out))
+                return 0
+            except Exception:  # noqa: BLE001 -- reported to the library as a failed exchange
+                return 1
+        cfn = _AllgatherFn(cb)
+        h = C.c_void_p()
+        _check(N.load().tns_comm_create_callback(rank, size, C.cast(cfn, C.c_void_p), None, C.byref(h)))
+        return cls(h, rank, size, keep=cfn)
+
+    @classmethod
+    def torch(cls, group=None, device=None) -> "Comm":
+        """Allgather through an initialised torch.distributed process group (nccl = RCCL on
+        ROCm, or gloo)."""
+        import torch
+        import torch.distributed as dist
+
+        rank, size = dist.get_rank(group), dist.get_world_size(group)
+
+        def fn(data: bytes) -> bytes:
+            t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+            if device is not None:
+                t = t.to(device)
+            out = torch.empty(len(data) * size, dtype=torch.uint8, device=t.device)
+            dist.all_gather_into_tensor(out, t, group=group)
+            return out.cpu().numpy().tobytes()
+        return cls.from_allgather(rank, size, fn)
+
+    def __del__(self):
+        try:
+            N.load().tns_comm_destroy(self.handle)
+        except Exception:
+            pass
+
+
+def setup_params_shard(log_size: int, rank: int, size: int, device: int = 0,
+                       ctx: Optional[Context] = None) -> Tuple[ProverParams, VerifierParams]:
+    """setup_params for rank `rank` of `size`: same params and tau; the SRS holds only this
+    rank's contiguous share of g1_powers."""
+    ctx = ctx or Context.get(device)
+    raw = N.TnsParams()
+    h = C.c_void_p()
+    _check(N.load().tns_setup_params_shard(ctx.handle, log_size, rank, size, C.byref(raw), C.byref(h)))
+    tau = from_mont(np.array(list(raw.tau), dtype=np.uint64))[0]
+    seed = bytes(raw.fiat_shamir_seed)
+    cp = CommitmentParams(Srs(ctx, h), tau)
+    pp = ProverParams(int(raw.log_size), int(raw.max_operations), cp, seed, raw)
+    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed)
+
+
+def shard_slice(n_total: int, rank: int, size: int) -> Tuple[int, int]:
+    """(first, count) of rank's slice of an n_total-entry vector padded to a power of two."""
+    L = (1 << max(0, (n_total - 1).bit_length())) // size
+    first = rank * L
+    return first, max(0, min(L, n_total - first))
+
+
+def twist_prove_sharded_resident(pp: ProverParams, comm: Comm, addr: DeviceBuffer, value: DeviceBuffer,
+                                 is_write: DeviceBuffer, n_local: int, n_total: int) -> N.TnsProof:
+    srs = pp.commitment_params.srs
+    pr = N.TnsProof()
+    _check(N.load().tns_twist_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, addr.ptr,
+                                            value.ptr, is_write.ptr, n_local, n_total, C.byref(pr)))
+    return pr
+
+
+def shout_prove_sharded_resident(pp: ProverParams, comm: Comm, entries: DeviceBuffer, n_entries: int,
+                                 n_entries_total: int, indices: DeviceBuffer, n_lookups: int,
+                                 n_lookups_total: int) -> N.TnsProof:
+    srs = pp.commitment_params.srs
+    pr = N.TnsProof()
+    _check(N.load().tns_shout_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, entries.ptr,
+                                            n_entries, n_entries_total, indices.ptr, n_lookups, n_lookups_total,
+                                            C.byref(pr)))
+    return pr
+
+
+def twist_proof_from_raw(pr: N.TnsProof) -> "TwistProof":
+    u = _unpack_proof(pr, 3)
+    return TwistProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"], u["z"], u["chals"], u["mle"])
+
+
+def shout_proof_from_raw(pr: N.TnsProof) -> "ShoutProof":
+    u = _unpack_proof(pr, 1)
+    return ShoutProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"], u["z"], u["chals"])
+
+
+def _nonempty_buf(ctx: Context, a: np.ndarray, dtype, width: int = 1) -> DeviceBuffer:
+    a = np.ascontiguousarray(a, dtype=dtype)
+    if a.size == 0:
+        a = np.zeros(width, dtype=dtype)
+    return DeviceBuffer(ctx, a)
+
+
+def bench_trace_slice(memory_size: int, n_total: int, first: int, count: int):
+    """Operations [first, first + count) of the n_total-op ProtocolBenchmarks trace."""
+    addr = np.empty(count, dtype=np.uint64)
+    val = np.empty(count, dtype=np.uint64)
+    isw = np.empty(count, dtype=np.uint8)
+    if count:
+        _check(N.load().tns_bench_trace_slice(memory_size, n_total, first, count, N.p64(addr), N.p64(val),
+                                              N.p8(isw)))
+    return addr, fr_from_u64_array(val), isw
+
+
 def profile_enable(ctx: Context, on: bool = True):
     N.load().tns_profile_enable(ctx.handle, 1 if on else 0)
 
@@ -782,5 +939,6 @@ __all__ = [
     "CommitmentParams", "ProverParams", "VerifierParams", "setup_params", "Transcript", "KZGCommitment",
     "KZGCommitmentValue", "KZGProof", "msm", "poly_utils", "MultilinearExtension", "SumCheck", "SumCheckProof",
     "MemoryOp", "MemoryTrace", "Twist", "TwistProof", "LookupOp", "LookupTable", "Shout", "ShoutProof",
-    "bench_trace", "to_mont", "from_mont", "fr_from_u64_array", "device_count",
+    "bench_trace", "to_mont", "from_mont", "fr_from_u64_array", "device_count", "Comm", "setup_params_shard",
+    "shard_slice", "bench_trace_slice",
 ]

@@ -119,6 +119,19 @@ SIGNATURES = [
     ("tns_fr_to_canonical", None, [U64P, C.c_size_t, U64P]),
     ("tns_fq_to_canonical", None, [U64P, C.c_size_t, U64P]),
     ("tns_bench_trace", C.c_int, [C.c_size_t, C.c_size_t, U64P, U64P, U8P]),
+    ("tns_bench_trace_slice", C.c_int, [C.c_size_t, C.c_uint64, C.c_uint64, C.c_size_t, U64P, U64P, U8P]),
+    ("tns_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("tns_comm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
+    ("tns_comm_create_callback", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("tns_comm_destroy", None, [C.c_void_p]),
+    ("tns_setup_params_shard", C.c_int,
+     [C.c_void_p, C.c_uint, C.c_int, C.c_int, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),
+    ("tns_twist_prove_sharded", C.c_int,
+     [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+      C.c_uint64, C.POINTER(TnsProof)]),
+    ("tns_shout_prove_sharded", C.c_int,
+     [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64, C.c_void_p,
+      C.c_size_t, C.c_uint64, C.POINTER(TnsProof)]),
     ("tns_last_prove_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
 ]
 

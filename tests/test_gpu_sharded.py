@@ -1,0 +1,177 @@
+"""One Twist / Shout proof sharded over ranks (BASELINE C5) on one MI355X.
+
+The ranks are threads, each with its own tns context, SRS shard (setup_params_shard) and
+slice of the trace; the allgather runs through the host-callback communicator, so the
+exchange protocol of the multi-GPU prover (partial MSM sums, barycentric partials, folded
+table values) is exercised end to end.  Every rank must return exactly the unsharded proof.
+The RCCL transport is covered with one rank (more need more GPUs).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import twist_and_shout as ts
+
+pytestmark = pytest.mark.gpu
+
+_PARAMS = {}
+
+
+def params(L):
+    """The unsharded ProverParams for setup_params(L)."""
+    if L not in _PARAMS:
+        _PARAMS[L] = ts.setup_params(L)[0]
+    return _PARAMS[L]
+
+
+class ThreadGather:
+    def __init__(self, size):
+        self.size = size
+        self.bar = threading.Barrier(size, timeout=120)
+        self.slots = [None] * size
+
+    def fn(self, rank):
+        def f(data):
+            self.slots[rank] = data
+            self.bar.wait()
+            out = b"".join(self.slots)
+            self.bar.wait()
+            return out
+        return f
+
+
+def run_ranks(size, body):
+    g = ThreadGather(size)
+    results, errors = [None] * size, [None] * size
+
+    def worker(r):
+        try:
+            comm = ts.Comm.from_allgather(r, size, g.fn(r))
+            results[r] = body(r, comm, ts.Context(0))
+        except BaseException as e:  # noqa: BLE001 -- surfaced below
+            errors[r] = e
+            g.bar.abort()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(size)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    return results, errors
+
+
+def sharded_twist(L, size, addr, val, isw):
+    n_total = len(addr)
+
+    def body(r, comm, ctx):
+        pp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+        first, count = ts.shard_slice(n_total, r, size)
+        return ts.Twist(pp).prove_sharded(comm, addr[first:first + count], val[first:first + count],
+                                          isw[first:first + count], n_total)
+    return run_ranks(size, body)
+
+
+@pytest.mark.parametrize("logn,size", [(3, 2), (3, 8), (4, 4), (10, 2), (10, 4), (12, 8), (14, 2)])
+def test_twist_sharded_equals_unsharded(logn, size):
+    L = max(1, logn - 2)
+    addr, val, isw = ts.bench_trace(1 << L, 1 << logn)
+    want = ts.Twist(params(L)).prove_soa(addr, val, isw)
+    got, errs = sharded_twist(L, size, addr, val, isw)
+    assert errs == [None] * size
+    for p in got:
+        assert p == want
+
+
+@pytest.mark.parametrize("n_total,size", [(1000, 4), (513, 2), (5, 4)])
+def test_twist_sharded_ragged_trace(n_total, size):
+    L = max(1, (n_total - 1).bit_length() - 2 + 1)
+    addr, val, isw = ts.bench_trace(1 << max(1, L - 1), n_total)
+    want = ts.Twist(params(L)).prove_soa(addr, val, isw)
+    got, errs = sharded_twist(L, size, addr, val, isw)
+    assert errs == [None] * size
+    assert all(p == want for p in got)
+
+
+def test_bench_trace_slices_concatenate():
+    a, v, w = ts.bench_trace(1 << 6, 3000)
+    parts = [ts.bench_trace_slice(1 << 6, 3000, f, c) for f, c in ((0, 1000), (1000, 1500), (2500, 500))]
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), a)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]), v)
+    assert np.array_equal(np.concatenate([p[2] for p in parts]), w)
+
+
+@pytest.mark.parametrize("T,M,size", [(8, 8, 2), (5, 3, 2), (64, 1000, 4), (4096, 17, 8), (1000, 4096, 4)])
+def test_shout_sharded_equals_unsharded(T, M, size):
+    L = 10
+    rng = np.random.default_rng(T + 7 * M)
+    entries = ts.to_mont([int(x) for x in rng.integers(0, 2**62, size=T)])
+    idx = rng.integers(0, T, size=M, dtype=np.uint64)
+    want = ts.Shout(params(L)).prove_arrays(entries, idx)
+
+    def body(r, comm, ctx):
+        pp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+        fe, ce = ts.shard_slice(T, r, size)
+        fi, ci = ts.shard_slice(M, r, size)
+        return ts.Shout(pp).prove_sharded(comm, entries[fe:fe + ce], T, idx[fi:fi + ci], M)
+    got, errs = run_ranks(size, body)
+    assert errs == [None] * size
+    assert all(p == want for p in got)
+
+
+def test_shout_sharded_bad_index_fails_on_every_rank():
+    L, T, M, size = 6, 16, 16, 2
+    entries = ts.to_mont(list(range(T)))
+    idx = np.arange(M, dtype=np.uint64)
+    idx[3] = T  # out of bounds, held by rank 0 only
+
+    def body(r, comm, ctx):
+        pp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+        fe, ce = ts.shard_slice(T, r, size)
+        fi, ci = ts.shard_slice(M, r, size)
+        return ts.Shout(pp).prove_sharded(comm, entries[fe:fe + ce], T, idx[fi:fi + ci], M)
+    _, errs = run_ranks(size, body)
+    assert all(isinstance(e, ts.InvalidParameters) for e in errs)
+
+
+def test_sharded_shape_errors():
+    L = 4
+    addr, val, isw = ts.bench_trace(16, 64)
+
+    def wrong_count(r, comm, ctx):
+        pp, _ = ts.setup_params_shard(L, r, 2, ctx=ctx)
+        return ts.Twist(pp).prove_sharded(comm, addr[:10], val[:10], isw[:10], 64)
+    _, errs = run_ranks(2, wrong_count)
+    assert all(isinstance(e, ts.InvalidParameters) for e in errs)
+
+    def three_ranks(r, comm, ctx):
+        pp, _ = ts.setup_params_shard(L, r, 3, ctx=ctx)
+        return ts.Twist(pp).prove_sharded(comm, addr[:22], val[:22], isw[:22], 64)
+    _, errs = run_ranks(3, three_ranks)
+    assert all(isinstance(e, ts.InvalidParameters) for e in errs)
+
+
+def test_setup_params_shard_splits_the_srs():
+    L, size = 3, 4
+    full = params(L).commitment_params.g1_powers  # 33 points
+    got = []
+    for r in range(size):
+        pp, _ = ts.setup_params_shard(L, r, size)
+        assert len(pp.commitment_params.srs) == len(full)
+        assert pp.commitment_params.tau == params(L).commitment_params.tau
+        got.append(pp)
+    # shards are disjoint and cover g1_powers (downloads are only allowed on the rank-0 shard)
+    first = got[0].commitment_params.srs
+    pts = first.download(8)
+    assert [(ts.from_mont(pts[i:i + 1, :4], ts.P_MOD)[0], ts.from_mont(pts[i:i + 1, 4:], ts.P_MOD)[0])
+            for i in range(8)] == full[:8]
+
+
+def test_rccl_communicator_one_rank():
+    L = 6
+    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
+    want = ts.Twist(params(L)).prove_soa(addr, val, isw)
+    ctx = ts.Context(0)
+    comm = ts.Comm.rccl(ctx, 0, 1, ts.Comm.unique_id())
+    pp, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
+    assert ts.Twist(pp).prove_sharded(comm, addr, val, isw, len(addr)) == want
