@@ -45,6 +45,13 @@ def parse():
     ap.add_argument("--commit-basis", choices=["lagrange", "coefficients"], default="lagrange",
                     help="prove via the setup's Lagrange-basis SRS (default) or via interpolation + "
                          "coefficient KZG (the reference's route); identical proofs")
+    ap.add_argument("--independent", action="store_true",
+                    help="N>1: one independent trace per rank instead of one trace sharded over the ranks")
+    ap.add_argument("--comm", choices=["torch", "rccl"], default="torch",
+                    help="sharded proof exchange: torch.distributed process group (nccl = RCCL) or the "
+                         "library's own RCCL communicator")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="testing aid: every rank on device 0 with a gloo process group (one-GPU box)")
     ap.add_argument("--no-msm-tables", action="store_true",
                     help="per-window MSM buckets instead of the fixed-base window tables")
     return ap.parse_args()
@@ -53,13 +60,13 @@ def parse():
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        if torch.cuda.is_available():
+        if torch.cuda.is_available() and not args.rehearse_one_gpu:
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", rank=rank, world_size=world)
         else:
@@ -82,7 +89,8 @@ def max_over_ranks(pg, local, x):
         return x
     import torch
 
-    dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+    on_gpu = torch.cuda.is_available() and pg.get_backend() == "nccl"
+    dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     pg.all_reduce(t, op=pg.ReduceOp.MAX)
     return float(t.item())
@@ -143,43 +151,77 @@ def main():
 
     ctx = ts.Context.get(local)
     log_ops = args.log_ops
-    n_ops = 1 << log_ops
-    L = log_ops - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
+    n_ops = 1 << log_ops  # per GPU
+    sharded = world > 1 and not args.independent
+    n_total = world * n_ops if sharded else n_ops  # operations of one proof
+    L = (n_total.bit_length() - 1) - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
     ctx.set_commit_basis(args.commit_basis == "lagrange")
     ctx.set_msm_tables(not args.no_msm_tables)
     t_setup = time.perf_counter()
-    pp, _ = ts.setup_params(L, device=local)
+    if sharded:  # one trace over all ranks: SRS share + basis slice per rank
+        pp, _ = ts.setup_params_shard(L, rank, world, ctx=ctx)
+    else:
+        pp, _ = ts.setup_params(L, device=local)
     t_setup = time.perf_counter() - t_setup
     t_lag = time.perf_counter()
     if args.commit_basis == "lagrange":  # setup-time product, like g1_powers (not proving work)
-        pp.commitment_params.srs.prepare_lagrange(n_ops)
+        if sharded:
+            pp.commitment_params.srs.prepare_lagrange_shard(n_total, rank, world)
+        else:
+            pp.commitment_params.srs.prepare_lagrange(n_ops)
     t_lag = time.perf_counter() - t_lag
-    addr, val, isw = ts.bench_trace(1 << L, n_ops)
+    if sharded:
+        first, count = ts.shard_slice(n_total, rank, world)
+        addr, val, isw = ts.bench_trace_slice(1 << L, n_total, first, count)
+        if args.comm == "rccl":
+            uid = [ts.Comm.unique_id() if rank == 0 else None]
+            pg.broadcast_object_list(uid, src=0)
+            comm = ts.Comm.rccl(ctx, rank, world, uid[0])
+        else:
+            import torch
+
+            on_gpu = torch.cuda.is_available() and not args.rehearse_one_gpu
+            comm = ts.Comm.torch(device=torch.device("cuda", local) if on_gpu else None)
+    else:
+        count = n_ops
+        addr, val, isw = ts.bench_trace(1 << L, n_ops)
     d_addr, d_val, d_isw = ts.DeviceBuffer(ctx, addr), ts.DeviceBuffer(ctx, val), ts.DeviceBuffer(ctx, isw)
 
+    def prove():
+        if sharded:
+            return ts.twist_prove_sharded_resident(pp, comm, d_addr, d_val, d_isw, count, n_total)
+        return ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
+
     for _ in range(args.warmup):
-        ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
+        prove()
     barrier_sync(pg, local)
     ts.profile_enable(ctx, True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
+        prove()
     barrier_sync(pg, local)
     dt = time.perf_counter() - t0
     breakdown = ctx.timing()
     roof, stages = roofline_from_profile(ts, ctx)
     ts.profile_enable(ctx, False)
     dt_max = max_over_ranks(pg, local, dt)
-    total_ops = world * n_ops * args.steps
+    total_ops = (n_total if sharded else world * n_ops) * args.steps
     value = total_ops / dt_max
+    if sharded:
+        workload = (f"C5-style: ONE Twist::prove of a {n_total}-op trace (2^{log_ops} per GPU) sharded over "
+                    f"{world} GPUs, setup_params_shard({L}), slices resident in HBM")
+        parallelism = f"one proof sharded x{world} ({args.comm} allgather of partial sums)"
+    else:
+        workload = f"C4: Twist::prove, 2^{log_ops}-op trace, setup_params({L}), trace resident in HBM"
+        parallelism = f"independent traces x{world}"
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u256 (8x u32 Montgomery, BN254 Fr/Fq)",
         "data": "synthetic (src/benchmarks.rs:88-99 trace)",
-        "config": {"workload": f"C4: Twist::prove, 2^{log_ops}-op trace, setup_params({L}), trace resident in HBM",
-                   "log_ops": log_ops, "ops_per_gpu": n_ops, "parallelism": f"independent traces x{world}"},
+        "config": {"workload": workload, "log_ops": log_ops, "ops_per_gpu": n_ops, "ops_per_proof": n_total,
+                   "parallelism": parallelism},
         "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
         "commit_basis": args.commit_basis,
         "setup_ms": {"setup_params": round(t_setup * 1e3, 1), "lagrange_basis": round(t_lag * 1e3, 1)},

@@ -230,6 +230,12 @@ int tns_comm_create(tns_ctx *ctx, int rank, int size, const uint8_t uid[128], tn
 /* Communicator over any host-side transport. */
 int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user, tns_comm **out);
 void tns_comm_destroy(tns_comm *comm);
+/* The communicator's allgather on its own (self-test / launcher use); ctx may be NULL for a
+ * callback communicator. */
+int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv);
+/* Build (and cache) rank `rank` of `size`'s slice of the Lagrange basis for N = 2^k nodes
+ * ahead of the first sharded proof of that size (setup, like tns_srs_prepare_lagrange). */
+int tns_srs_prepare_lagrange_shard(tns_ctx *ctx, tns_srs *srs, size_t n, int rank, int size);
 /* setup_params for rank `rank` of `size`: the same params/tau as tns_setup_params, with the
  * SRS holding only its contiguous share of g1_powers (the "SRS shard generated locally from
  * tau"); tns_srs_len still reports the full length. */

@@ -912,6 +912,30 @@ int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user
 
 void tns_comm_destroy(tns_comm *comm) { delete comm; }
 
+int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv) {
+  return guarded([&]() {
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    comm->c->allgather(ctx ? &ctx->c : nullptr, send, bytes, recv);
+    return TNS_OK;
+  });
+}
+
+int tns_srs_prepare_lagrange_shard(tns_ctx *ctx, tns_srs *srs, size_t n, int rank, int size) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    if (!srs->s.has_tau) throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS has no tau");
+    if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
+    if (size < 1 || (size & (size - 1)) || rank < 0 || rank >= size || (size_t)size > n)
+      throw Error(TNS_ERR_INVALID_PARAMETERS, "bad shard");
+    const bool saved = ctx->c.lagrange_commit;
+    ctx->c.lagrange_commit = true;
+    const size_t L = n / size;
+    (void)lagrange_basis_dev(&ctx->c, srs->s, n, (size_t)rank * L, L);
+    ctx->c.lagrange_commit = saved;
+    return TNS_OK;
+  });
+}
+
 // ---------------------------------------------------------------- device buffers
 int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer **out) {
   return guarded([&]() {

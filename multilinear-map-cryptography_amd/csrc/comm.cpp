@@ -49,6 +49,7 @@ struct RcclComm final : Comm {
     if (comm) (void)ncclCommDestroy(comm);
   }
   void allgather(Ctx *c, const void *send, size_t bytes, void *recv) override {
+    if (!c) throw Error(TNS_ERR_INVALID_PARAMETERS, "the RCCL communicator needs a context");
     void *ds = send_b.ensure(bytes ? bytes : 1), *dr = recv_b.ensure(bytes * size ? bytes * size : 1);
     TNS_HIP(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, c->stream));
     TNS_NCCL(ncclAllGather(ds, dr, bytes, ncclUint8, comm, c->stream));

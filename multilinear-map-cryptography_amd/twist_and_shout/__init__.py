@@ -176,6 +176,10 @@ class Srs:
         """Attach the setup trapdoor (CommitmentParams.tau) so the Lagrange basis exists."""
         _check(N.load().tns_srs_set_tau(self.handle, N.p64(to_mont([tau]))))
 
+    def prepare_lagrange_shard(self, n: int, rank: int, size: int):
+        """Build rank's slice of the Lagrange basis for n nodes (sharded proving setup)."""
+        _check(N.load().tns_srs_prepare_lagrange_shard(self.ctx.handle, self.handle, n, rank, size))
+
     def prepare_lagrange(self, n: int):
         """Build the Lagrange basis for n = 2^k nodes now (setup time) instead of at the
         first proof of that size."""
@@ -820,6 +824,13 @@ class Comm:
             dist.all_gather_into_tensor(out, t, group=group)
             return out.cpu().numpy().tobytes()
         return cls.from_allgather(rank, size, fn)
+
+    def allgather(self, data: bytes, ctx: Optional[Context] = None) -> bytes:
+        """The communicator's own allgather (every rank's bytes, in rank order)."""
+        src = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+        out = (C.c_uint8 * max(1, len(data) * self.size))()
+        _check(N.load().tns_comm_allgather(ctx.handle if ctx else None, self.handle, src, len(data), out))
+        return bytes(out)[:len(data) * self.size]
 
     def __del__(self):
         try:

@@ -124,6 +124,8 @@ SIGNATURES = [
     ("tns_comm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
     ("tns_comm_create_callback", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("tns_comm_destroy", None, [C.c_void_p]),
+    ("tns_comm_allgather", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    ("tns_srs_prepare_lagrange_shard", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]),
     ("tns_setup_params_shard", C.c_int,
      [C.c_void_p, C.c_uint, C.c_int, C.c_int, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),
     ("tns_twist_prove_sharded", C.c_int,
