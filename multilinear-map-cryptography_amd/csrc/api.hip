@@ -43,6 +43,8 @@ void set_last_error(const std::string &m) { g_last_error = m; }
 Ctx::~Ctx() {
   for (auto *p : plans) delete p;
   for (auto &kv : pass_tw) delete kv.second;
+  for (auto &kv : bary_w) delete kv.second;
+  if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -165,6 +167,68 @@ static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *val
   open_dev(c, srs, p.coeffs, p.N, z, value, proof, sbuf);
 }
 
+// Both vectors of a proof at once (the two commitments; the two openings at the same z):
+// their MSMs overlap on the context's two lanes and each exchange step carries both.
+static G1Xyzz sum_rank_parts(const G1Xyzz *all, int size, int stride, int k) {
+  G1Xyzz acc = G1Xyzz::inf();
+  for (int r = 0; r < size; r++) acc = xyzz_add(acc, all[(size_t)r * stride + k]);
+  return acc;
+}
+
+static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affine out[2]) {
+  if (m.size == 1) {
+    out[0] = xyzz_to_affine(part[0]);
+    out[1] = xyzz_to_affine(part[1]);
+    return;
+  }
+  std::vector<G1Xyzz> all(2 * (size_t)m.size);
+  m.allgather(c, part, 2 * sizeof(G1Xyzz), all.data());
+  out[0] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 0));
+  out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 1));
+}
+
+static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, Comm &m, G1Affine out[2]) {
+  if (p0.N > srs.n || p1.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+  p0.basis = lagrange_basis_dev(c, srs, p0.N, p0.first, p0.cnt);
+  p1.basis = lagrange_basis_dev(c, srs, p1.N, p1.first, p1.cnt);
+  if (!p0.basis || !p1.basis) {
+    out[0] = commit_evals(c, srs, p0, m);
+    out[1] = commit_evals(c, srs, p1, m);
+    return;
+  }
+  G1Xyzz part[2];
+  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), p0.y, p0.cnt, p0.basis->fb},
+               MsmArgs{p1.basis->points.as<G1Affine>(), p1.y, p1.cnt, p1.basis->fb}, part);
+  allgather_sum_g1_pair(c, m, part, out);
+}
+
+static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, const Fr &z, Fr value[2],
+                            G1Affine proof[2], DevBuf &sbuf0, DevBuf &sbuf1, Comm &m) {
+  if (!p0.basis || !p1.basis || fr_is_node(z, p0.N) || fr_is_node(z, p1.N)) {
+    open_evals(c, srs, p0, z, &value[0], &proof[0], sbuf0, m);
+    open_evals(c, srs, p1, z, &value[1], &proof[1], sbuf0, m);
+    return;
+  }
+  Fr *q0 = (Fr *)sbuf0.ensure(sizeof(Fr) * p0.cnt), *q1 = (Fr *)sbuf1.ensure(sizeof(Fr) * p1.cnt);
+  Fr part[4];
+  lagrange_open_partial_dev(c, p0.y, p0.N, p0.first, p0.cnt, z, q0, &part[0], &part[1]);
+  lagrange_open_partial_dev(c, p1.y, p1.N, p1.first, p1.cnt, z, q1, &part[2], &part[3]);
+  Fr ell[2] = {Fr::one(), Fr::one()}, S[2] = {Fr::zero(), Fr::zero()};
+  const std::vector<Fr> all = allgather_fr(c, m, part, 4);
+  for (int r = 0; r < m.size; r++)
+    for (int k = 0; k < 2; k++) {
+      ell[k] = mul(ell[k], all[4 * (size_t)r + 2 * k]);
+      S[k] = add(S[k], all[4 * (size_t)r + 2 * k + 1]);
+    }
+  for (int k = 0; k < 2; k++) value[k] = mul(ell[k], S[k]);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
+  lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
+  lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
+  G1Xyzz pp[2];
+  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb},
+               MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb}, pp);
+  allgather_sum_g1_pair(c, m, pp, proof);
+}
+
 // shard geometry: `size` ranks over N padded entries (size a power of two <= N)
 static void check_shard(const Comm &m, size_t N, const char *what) {
   if (m.size & (m.size - 1)) throw Error(TNS_ERR_INVALID_PARAMETERS, "rank count must be a power of two");
@@ -222,6 +286,8 @@ int tns_ctx_create(int device, tns_ctx **out) {
     tns_ctx *x = new tns_ctx();
     x->c.device = device;
     TNS_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
+    x->c.lanes[0].stream = x->c.stream;
+    TNS_HIP(hipStreamCreateWithFlags(&x->c.lanes[1].stream, hipStreamNonBlocking));
     *out = x;
     return TNS_OK;
   });
@@ -623,14 +689,13 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
       (void)tr.challenge(lab);
     }
     std::memcpy(out->opening_point, &z, 32);
-    Fr va, vb;
-    G1Affine pa, pb;
-    open_evals(c, srs, polyA, z, &va, &pa, sbuf, m);
-    open_evals(c, srs, polyB, z, &vb, &pb, sbuf, m);
-    store_proj(pa, out->opening_proofs[0]);
-    store_proj(pb, out->opening_proofs[1]);
-    std::memcpy(out->final_evaluations[0], &va, 32);
-    std::memcpy(out->final_evaluations[1], &vb, 32);
+    Fr v[2];
+    G1Affine pi[2];
+    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m);
+    store_proj(pi[0], out->opening_proofs[0]);
+    store_proj(pi[1], out->opening_proofs[1]);
+    std::memcpy(out->final_evaluations[0], &v[0], 32);
+    std::memcpy(out->final_evaluations[1], &v[1], 32);
     out->num_openings = 2;
   }
   timing[4] = t_open.ms();
@@ -711,8 +776,9 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   pv.y = YV;
   tm[1] = t_int.ms();
   Timer t_com;
-  G1Affine Ca = commit_evals(c, srs->s, pa, m);
-  G1Affine Cv = commit_evals(c, srs->s, pv, m);
+  G1Affine cm[2];
+  commit_evals_pair(c, srs->s, pa, pv, m, cm);
+  const G1Affine Ca = cm[0], Cv = cm[1];
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
   tm[2] = t_com.ms();
@@ -827,8 +893,9 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   pi.y = YI;
   tm[1] = t_int.ms();
   Timer t_com;
-  G1Affine Ct = commit_evals(c, srs->s, pt, m);  // table first (src/shout.rs:125-133)
-  G1Affine Ci = commit_evals(c, srs->s, pi, m);
+  G1Affine cm[2];
+  commit_evals_pair(c, srs->s, pt, pi, m, cm);  // table first (src/shout.rs:125-133)
+  const G1Affine Ct = cm[0], Ci = cm[1];
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);
   tm[2] = t_com.ms();

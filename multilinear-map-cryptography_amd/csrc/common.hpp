@@ -70,6 +70,37 @@ struct DevBuf {
   }
 };
 
+// Grow-only pinned host buffer (async device-to-host readbacks).
+struct PinnedBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  PinnedBuf() = default;
+  PinnedBuf(const PinnedBuf &) = delete;
+  PinnedBuf &operator=(const PinnedBuf &) = delete;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void *ensure(size_t n) {
+    if (n <= bytes && p) return p;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault);
+    if (e != hipSuccess) throw Error(TNS_ERR_OOM, std::string("hipHostMalloc failed: ") + hipGetErrorString(e));
+    bytes = n ? n : 16;
+    return p;
+  }
+};
+
+// One stream's MSM workspaces (msm.hip): two lanes let two independent MSMs of a proof
+// (the two commitments, the two opening quotients) overlap on the device.
+struct MsmLane {
+  hipStream_t stream = nullptr;
+  DevBuf ws[10];
+  DevBuf fix;       // heavy-bucket level sums
+  PinnedBuf host;   // scalar bit length, then the per-set sums
+};
+
 // Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).
 struct InterpPlan {
   unsigned log_n = 0;   // N = 2^log_n
@@ -176,9 +207,8 @@ struct Ctx {
   std::mutex mu;
   // workspaces
   DevBuf scratch[8];
-  DevBuf msm_ws[10];
-  DevBuf fix_ws;        // MSM heavy-bucket level sums
-  DevBuf prove_ws[12];  // resident trace / coefficient vectors of Twist/Shout::prove
+  MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
+  DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
   DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
@@ -194,6 +224,8 @@ struct Ctx {
 // TNS_PROF(ctx, "stage", algorithmic_bytes_of_this_launch)
 #define TNS_PROF(ctx, name, bytes) \
   ::tns::ProfScope TNS_CAT(_tns_prof_, __LINE__)((ctx)->prof, (ctx)->stream, name, (double)(bytes))
+#define TNS_PROF_ON(ctx, stream, name, bytes) \
+  ::tns::ProfScope TNS_CAT(_tns_prof_, __LINE__)((ctx)->prof, stream, name, (double)(bytes))
 
 // RAII device guard + lock
 struct CtxScope {
@@ -247,6 +279,14 @@ void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
 G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr);
+struct MsmArgs {
+  const G1Affine *points;
+  const Fr *scalars;
+  size_t n;
+  const FixedBase *fb;
+};
+// two independent MSMs overlapped on the context's two lanes (inputs ready on c->stream)
+void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);

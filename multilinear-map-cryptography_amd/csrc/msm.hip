@@ -428,8 +428,7 @@ const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n) {
 
 // ---------------------------------------------------------------- driver
 // sum over each set of the sets x n array X (device) -> out (sets, device)
-static void sum_sets(Ctx *ctx, G1Xyzz *X, int sets, size_t n, G1Xyzz *tmp, G1Xyzz *out) {
-  hipStream_t st = ctx->stream;
+static void sum_sets(hipStream_t st, G1Xyzz *X, int sets, size_t n, G1Xyzz *tmp, G1Xyzz *out) {
   G1Xyzz *src = X, *dst = tmp;
   while (n > 128 && n % 8 == 0) {  // short chains: these passes are latency-bound
     const size_t n_out = (size_t)sets * (n / 8);
@@ -442,32 +441,53 @@ static void sum_sets(Ctx *ctx, G1Xyzz *X, int sets, size_t n, G1Xyzz *tmp, G1Xyz
   TNS_LAUNCH_CHECK();
 }
 
-G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb) {
-  if (n == 0) return G1Xyzz::inf();
-  hipStream_t st = ctx->stream;
+// One MSM in flight on a lane: launched by msm_launch, completed by msm_complete.
+struct MsmJob {
+  MsmLane *lane = nullptr;
+  bool immediate = false;  // result already known (n == 0, all scalars zero)
+  G1Xyzz result;
+  bool tiny = false;       // k_msm_tiny path: one point in the lane's pinned buffer
+  MsmPlan P;
+  int L0 = 0, nbits = 0, specs = 0;
+};
+
+static void bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
+  unsigned *d_bits = (unsigned *)ln.ws[4].ensure(sizeof(unsigned));
+  unsigned *h_bits = (unsigned *)ln.host.ensure(sizeof(unsigned));
+  TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), ln.stream));
+  k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
+}
+
+static unsigned bits_result(MsmLane &ln) {
+  TNS_HIP(hipStreamSynchronize(ln.stream));
+  return *(unsigned *)ln.host.p;
+}
+
+// Enqueue everything up to the per-set sums' readback on lane `ln` (asynchronous).
+static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
+                       const FixedBase *fb, unsigned bits, MsmJob &J) {
+  J.lane = &ln;
+  hipStream_t st = ln.stream;
+  if (n == 0 || bits == 0) {  // all scalars zero
+    J.immediate = true;
+    J.result = G1Xyzz::inf();
+    return;
+  }
   if (n <= 64) {
-    G1Xyzz *d = (G1Xyzz *)ctx->msm_ws[0].ensure(sizeof(G1Xyzz));
+    G1Xyzz *d = (G1Xyzz *)ln.ws[0].ensure(sizeof(G1Xyzz));
     k_msm_tiny<<<1, 64, 0, st>>>(points, scalars, (int)n, d);
     TNS_LAUNCH_CHECK();
-    G1Xyzz h;
-    TNS_HIP(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, st));
-    TNS_HIP(hipStreamSynchronize(st));
-    return h;
+    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz)), d, sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+    J.tiny = true;
+    return;
   }
   if (n >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM larger than 2^31 points");
-  unsigned bits = 0;
-  {
-    unsigned *d_bits = (unsigned *)ctx->msm_ws[4].ensure(sizeof(unsigned));
-    TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), st));
-    k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, st>>>(scalars, n, d_bits);
-    TNS_LAUNCH_CHECK();
-    TNS_HIP(hipMemcpyAsync(&bits, d_bits, sizeof bits, hipMemcpyDeviceToHost, st));
-    TNS_HIP(hipStreamSynchronize(st));
-  }
-  if (bits == 0) return G1Xyzz::inf();  // all scalars zero
 
   // plan: per-window layout, or the shared layout when a fixed-base table covers the points
-  MsmPlan P;
+  MsmPlan &P = J.P;
+  P = MsmPlan();
   P.c = best_window(n, (int)bits, 20, false);
   P.W = windows_for((int)bits, P.c);
   if (fb && ctx->msm_tables && fb->n >= n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
@@ -484,18 +504,18 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
-  uint32_t *keys = (uint32_t *)ctx->msm_ws[0].ensure(sizeof(uint32_t) * total);
-  uint32_t *vals = (uint32_t *)ctx->msm_ws[1].ensure(sizeof(uint32_t) * total);
-  uint32_t *keys2 = (uint32_t *)ctx->msm_ws[2].ensure(sizeof(uint32_t) * total);
-  uint32_t *vals2 = (uint32_t *)ctx->msm_ws[3].ensure(sizeof(uint32_t) * total);
-  uint32_t *bounds = (uint32_t *)ctx->msm_ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
+  uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
+  uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
+  uint32_t *keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
+  uint32_t *vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
+  uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
   uint32_t *bstart = bounds, *bend = bounds + P.nb, *valid = bounds + 2 * P.nb;
-  G1Xyzz *buckets = (G1Xyzz *)ctx->msm_ws[5].ensure(sizeof(G1Xyzz) * P.nb);
+  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
   const size_t nchunks = (total + ACC_K - 1) / ACC_K;
-  HeadTail *ht = (HeadTail *)ctx->msm_ws[6].ensure(sizeof(HeadTail) * nchunks);
+  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
 
   {
-    TNS_PROF(ctx, "msm_digits", 32.0 * n + 8.0 * total);
+    TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
     k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
                                                keys, vals);
     TNS_LAUNCH_CHECK();
@@ -503,9 +523,9 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   size_t temp_bytes = 0;
   TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total,
                                              0, P.end_bit, st));
-  void *temp = ctx->msm_ws[9].ensure(temp_bytes);
+  void *temp = ln.ws[9].ensure(temp_bytes);
   {
-    TNS_PROF(ctx, "msm_sort", 16.0 * total);
+    TNS_PROF_ON(ctx, st, "msm_sort", 16.0 * total);
     TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
                                                P.end_bit, st));
     TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
@@ -513,14 +533,14 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
     TNS_LAUNCH_CHECK();
   }
   {
-    TNS_PROF(ctx, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
+    TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
     k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
                                                                    points, buckets, ht, nchunks);
     TNS_LAUNCH_CHECK();
   }
-  FixLevels F{};
   {
-    TNS_PROF(ctx, "msm_fixup", 0.0);
+    TNS_PROF_ON(ctx, st, "msm_fixup", 0.0);
+    FixLevels F{};
     size_t groups = nchunks / FIX_FAN, off = 0;
     while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/F, /F^2, ...
       F.len[F.n + 1] = groups;
@@ -529,7 +549,7 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
       F.n++;
     }
     if (F.n) {
-      G1Xyzz *base = (G1Xyzz *)ctx->fix_ws.ensure(sizeof(G1Xyzz) * off);
+      G1Xyzz *base = (G1Xyzz *)ln.fix.ensure(sizeof(G1Xyzz) * off);
       size_t o = 0;
       for (int l = 1; l <= F.n; l++) {
         F.lv[l] = base + o;
@@ -545,38 +565,46 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
   // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
   // as nbits + 1 plain sums (the M_b and sum_g T_g) -- short dependency chains only
-  std::vector<G1Xyzz> fin;
-  const int L0 = (int)std::min<size_t>(RED_L, P.half);
-  const size_t g = P.half / L0;
-  int nbits = 0;
-  while (((size_t)1 << nbits) < g) nbits++;
-  const int specs = nbits + 1;
+  J.L0 = (int)std::min<size_t>(RED_L, P.half);
+  const size_t g = P.half / J.L0;
+  J.nbits = 0;
+  while (((size_t)1 << J.nbits) < g) J.nbits++;
+  J.specs = J.nbits + 1;
   {
-    TNS_PROF(ctx, "msm_reduce", 128.0 * P.nb);
-    G1Xyzz *T = (G1Xyzz *)ctx->msm_ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * g);
+    TNS_PROF_ON(ctx, st, "msm_reduce", 128.0 * P.nb);
+    G1Xyzz *T = (G1Xyzz *)ln.ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * g);
     G1Xyzz *S = T + (size_t)P.Wr * g;
-    k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, L0, T, S);
+    k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
     TNS_LAUNCH_CHECK();
     const int CH = (int)std::min<size_t>(16, g);
     const size_t nch = g / CH;
-    const size_t nparts = (size_t)P.Wr * specs * nch;
-    G1Xyzz *parts = (G1Xyzz *)ctx->msm_ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * specs));
+    const size_t nparts = (size_t)P.Wr * J.specs * nch;
+    G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
     G1Xyzz *tmp = parts + nparts, *out = tmp + nparts;
-    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, nbits, CH, parts);
+    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, J.nbits, CH, parts);
     TNS_LAUNCH_CHECK();
-    sum_sets(ctx, parts, P.Wr * specs, nch, tmp, out);
-    fin.resize((size_t)P.Wr * specs);
-    TNS_HIP(hipMemcpyAsync(fin.data(), out, sizeof(G1Xyzz) * fin.size(), hipMemcpyDeviceToHost, st));
-    TNS_HIP(hipStreamSynchronize(st));
+    sum_sets(st, parts, P.Wr * J.specs, nch, tmp, out);
+    const size_t fin_n = (size_t)P.Wr * J.specs;
+    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz) * fin_n), out, sizeof(G1Xyzz) * fin_n,
+                           hipMemcpyDeviceToHost, st));
   }
-  // R = sum_g T_g + L0 * sum_b 2^b M_b  (host: ~nbits + 4 doublings per set)
+}
+
+// Wait for the lane and finish on the host: R = sum_g T_g + L0 * sum_b 2^b M_b per set,
+// then Horner over the windows (per-window layout).
+static G1Xyzz msm_complete(MsmJob &J) {
+  if (J.immediate) return J.result;
+  TNS_HIP(hipStreamSynchronize(J.lane->stream));
+  if (J.tiny) return *(const G1Xyzz *)J.lane->host.p;
+  const MsmPlan &P = J.P;
+  const G1Xyzz *fin = (const G1Xyzz *)J.lane->host.p;
   std::vector<G1Xyzz> Rw(P.Wr);
   for (int r = 0; r < P.Wr; r++) {
-    const G1Xyzz *f = &fin[(size_t)r * specs];
+    const G1Xyzz *f = &fin[(size_t)r * J.specs];
     G1Xyzz acc = G1Xyzz::inf();
-    for (int b = nbits - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), f[b]);
-    for (int L = L0; L > 1; L >>= 1) acc = xyzz_dbl(acc);
-    Rw[r] = xyzz_add(f[nbits], acc);
+    for (int b = J.nbits - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), f[b]);
+    for (int L = J.L0; L > 1; L >>= 1) acc = xyzz_dbl(acc);
+    Rw[r] = xyzz_add(f[J.nbits], acc);
   }
   if (P.shared) return Rw[0];
   G1Xyzz acc = Rw[P.W - 1];
@@ -585,6 +613,39 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
     acc = xyzz_add(acc, Rw[w]);
   }
   return acc;
+}
+
+G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb) {
+  if (n == 0) return G1Xyzz::inf();
+  MsmLane &ln = ctx->lanes[0];
+  unsigned bits = 254;
+  if (n > 64) {
+    bits_launch(ln, scalars, n);
+    bits = bits_result(ln);
+  }
+  MsmJob J;
+  msm_launch(ctx, ln, points, scalars, n, fb, bits, J);
+  return msm_complete(J);
+}
+
+void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
+  MsmLane &l0 = ctx->lanes[0], &l1 = ctx->lanes[1];
+  // lane 1 starts after everything already queued on the context stream (its inputs)
+  hipEvent_t ready;
+  TNS_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+  TNS_HIP(hipEventRecord(ready, ctx->stream));
+  TNS_HIP(hipStreamWaitEvent(l1.stream, ready, 0));
+  (void)hipEventDestroy(ready);
+  unsigned ba = 254, bb = 254;
+  if (a.n > 64) bits_launch(l0, a.scalars, a.n);
+  if (b.n > 64) bits_launch(l1, b.scalars, b.n);
+  if (a.n > 64) ba = bits_result(l0);
+  if (b.n > 64) bb = bits_result(l1);
+  MsmJob ja, jb;
+  msm_launch(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja);
+  msm_launch(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb);
+  out[0] = msm_complete(ja);
+  out[1] = msm_complete(jb);
 }
 
 }  // namespace tns
