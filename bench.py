@@ -32,6 +32,10 @@ import numpy as np  # noqa: E402
 
 METRIC = "Twist prover ops/sec + KZG MSM G1-scalar-pairs/sec at 2^20, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# v_mad_u64_u32 throughput of independent streams, measured by tools/mulbench2.hip on MI355X
+# (profiles/r01_mulbench2.txt): the integer-VALU ceiling of the MSM accumulation.
+MAC_PEAK_T = 28.61
+MACS_PER_MADD = 10 * 128  # madd-2008-s: 10 Fq products of 8x8 32-bit limbs (+ as many for the reduction)
 
 
 def parse():
@@ -121,7 +125,18 @@ def roofline_from_profile(ts, ctx):
             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
             "alg_bytes_per_launch": per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
             "note": "dominant stage by device time; integer-VALU-bound (256-bit Montgomery), so the HBM "
-                    "fraction is low by construction -- see DESIGN.md"}
+                    "fraction is low by construction (compute position: the 'compute' object); the two "
+                    "MSMs of each commit/open pair run concurrently on two streams, so a launch's duration "
+                    "includes its co-runner -- see DESIGN.md"}
+    ex = ts.profile_read_ex(ctx, "msm_accumulate")
+    if ex["ops"] and ex["busy_ms"]:
+        tmacs = ex["ops"] * MACS_PER_MADD / (ex["busy_ms"] / 1e3) / 1e12
+        roof["compute"] = {"kernel": "msm_accumulate", "bound": "valu (v_mad_u64_u32)", "unit": "T MAC/s",
+                           "achieved": round(tmacs, 3), "peak": MAC_PEAK_T, "frac": round(tmacs / MAC_PEAK_T, 4),
+                           "madds": ex["ops"], "busy_ms": round(ex["busy_ms"], 3),
+                           "note": "mixed additions x 1280 MACs over the union of the stage's launch intervals; "
+                                   "peak = measured independent v_mad_u64_u32 streams (tools/mulbench2.hip); the "
+                                   "carry instruction of each MAC bounds the reachable fraction near 0.7"}
     return roof, stages
 
 

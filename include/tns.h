@@ -262,6 +262,9 @@ int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *
 int tns_profile_enable(tns_ctx *ctx, int on);
 int tns_profile_read(tns_ctx *ctx, const char *stage, double *total_ms, uint64_t *launches,
                      double *algorithmic_bytes);
+/* out = {summed launch ms, launches, algorithmic bytes, operations (msm_accumulate: mixed
+ * additions), busy ms (union of the launch intervals: stages of the two MSM lanes overlap)} */
+int tns_profile_read_ex(tns_ctx *ctx, const char *stage, double out[5]);
 
 /* ---------------------------------------------------------------- host utilities (no device) */
 /* Batch conversions between integers and Montgomery-form Fr / Fq (multi-threaded). */

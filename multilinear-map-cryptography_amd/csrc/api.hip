@@ -1039,8 +1039,23 @@ int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, 
 // ---------------------------------------------------------------- kernel timing (HIP events)
 int tns_profile_enable(tns_ctx *ctx, int on) {
   ctx->c.prof.enabled = on != 0;
-  ctx->c.prof.reset();
+  ctx->c.prof.start(ctx->c.stream);
   return TNS_OK;
+}
+
+int tns_profile_read_ex(tns_ctx *ctx, const char *stage, double out[5]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.prof.collect();
+    auto it = ctx->c.prof.totals.find(stage);
+    const bool f = it != ctx->c.prof.totals.end();
+    out[0] = f ? it->second.ms : 0.0;
+    out[1] = f ? (double)it->second.launches : 0.0;
+    out[2] = f ? it->second.bytes : 0.0;
+    out[3] = f ? it->second.ops : 0.0;
+    out[4] = f ? it->second.busy_ms : 0.0;
+    return TNS_OK;
+  });
 }
 int tns_profile_read(tns_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches, double *alg_bytes) {
   return guarded([&]() {

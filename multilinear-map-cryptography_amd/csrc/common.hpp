@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -145,39 +146,68 @@ struct Srs {
   }
 };
 
-// Per-kernel device time from HIP events recorded on the context stream around
-// the launches of one named stage (enabled by tns_profile_enable; used by bench.py
-// for the roofline's live kernel duration).
+// Per-stage device time from HIP events recorded around the launches of one named stage
+// (enabled by tns_profile_enable; used by bench.py for the roofline's live kernel duration).
+// Besides the summed launch durations, each stage keeps the union of its launch intervals
+// (stages of two MSM lanes overlap) and an optional operation count (MSM mixed additions).
 struct KernelProfiler {
   bool enabled = false;
+  hipEvent_t ref = nullptr;  // recorded at enable: common time origin of every stream
   struct Rec {
     std::string name;
     hipEvent_t a, b;
     double bytes;
   };
   struct Tot {
-    double ms = 0, bytes = 0;
+    double ms = 0, bytes = 0, ops = 0, busy_ms = 0;
     uint64_t launches = 0;
+    std::vector<std::pair<double, double>> iv;
   };
   std::vector<Rec> pending;
-  std::map<std::string, Tot> totals;  // name -> (device ms, launches, algorithmic bytes)
+  std::map<std::string, Tot> totals;
+  void start(hipStream_t s) {
+    reset();
+    if (!ref) (void)hipEventCreate(&ref);
+    (void)hipEventRecord(ref, s);
+  }
   void reset() {
     collect();
     totals.clear();
   }
+  void add_ops(const char *name, double ops) {
+    if (enabled) totals[name].ops += ops;
+  }
   void collect() {
     for (auto &r : pending) {
-      float ms = 0.f;
+      float ms = 0.f, t0 = 0.f, t1 = 0.f;
       if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
         auto &t = totals[r.name];
         t.ms += ms;
         t.launches += 1;
         t.bytes += r.bytes;
+        if (ref && hipEventElapsedTime(&t0, ref, r.a) == hipSuccess && hipEventElapsedTime(&t1, ref, r.b) == hipSuccess)
+          t.iv.emplace_back(t0, t1);
       }
       (void)hipEventDestroy(r.a);
       (void)hipEventDestroy(r.b);
     }
     pending.clear();
+    for (auto &kv : totals) {  // union of the launch intervals
+      auto &iv = kv.second.iv;
+      std::sort(iv.begin(), iv.end());
+      double busy = 0, lo = -1, hi = -1;
+      for (auto &x : iv) {
+        if (x.first > hi) {
+          busy += hi - lo;
+          lo = x.first;
+          hi = x.second;
+        } else if (x.second > hi) {
+          hi = x.second;
+        }
+      }
+      busy += hi - lo;
+      kv.second.busy_ms = busy;
+    }
   }
 };
 

@@ -585,19 +585,22 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
     TNS_LAUNCH_CHECK();
     sum_sets(st, parts, P.Wr * J.specs, nch, tmp, out);
     const size_t fin_n = (size_t)P.Wr * J.specs;
-    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz) * fin_n), out, sizeof(G1Xyzz) * fin_n,
-                           hipMemcpyDeviceToHost, st));
+    char *h = (char *)ln.host.ensure(sizeof(G1Xyzz) * fin_n + 16);
+    TNS_HIP(hipMemcpyAsync(h, out, sizeof(G1Xyzz) * fin_n, hipMemcpyDeviceToHost, st));
+    // the number of sorted non-zero digits = mixed additions of k_accumulate (profiling)
+    TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   }
 }
 
 // Wait for the lane and finish on the host: R = sum_g T_g + L0 * sum_b 2^b M_b per set,
 // then Horner over the windows (per-window layout).
-static G1Xyzz msm_complete(MsmJob &J) {
+static G1Xyzz msm_complete(Ctx *ctx, MsmJob &J) {
   if (J.immediate) return J.result;
   TNS_HIP(hipStreamSynchronize(J.lane->stream));
   if (J.tiny) return *(const G1Xyzz *)J.lane->host.p;
   const MsmPlan &P = J.P;
   const G1Xyzz *fin = (const G1Xyzz *)J.lane->host.p;
+  ctx->prof.add_ops("msm_accumulate", (double)*(const uint32_t *)(fin + (size_t)P.Wr * J.specs));
   std::vector<G1Xyzz> Rw(P.Wr);
   for (int r = 0; r < P.Wr; r++) {
     const G1Xyzz *f = &fin[(size_t)r * J.specs];
@@ -625,7 +628,7 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   }
   MsmJob J;
   msm_launch(ctx, ln, points, scalars, n, fb, bits, J);
-  return msm_complete(J);
+  return msm_complete(ctx, J);
 }
 
 void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
@@ -644,8 +647,8 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   MsmJob ja, jb;
   msm_launch(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja);
   msm_launch(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb);
-  out[0] = msm_complete(ja);
-  out[1] = msm_complete(jb);
+  out[0] = msm_complete(ctx, ja);
+  out[1] = msm_complete(ctx, jb);
 }
 
 }  // namespace tns

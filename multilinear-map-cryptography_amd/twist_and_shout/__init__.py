@@ -917,6 +917,14 @@ PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_fixup", "msm_
                   "ntt_pointwise", "interp_tile", "interp_elementwise", "sumcheck_round", "open_scan"]
 
 
+def profile_read_ex(ctx: Context, stage: str) -> dict:
+    """Stage totals since profile_enable: summed launch ms, launches, algorithmic bytes,
+    operations (msm_accumulate: mixed additions) and busy ms (union of launch intervals)."""
+    out = (C.c_double * 5)()
+    _check(N.load().tns_profile_read_ex(ctx.handle, stage.encode(), out))
+    return dict(ms=out[0], launches=int(out[1]), bytes=out[2], ops=out[3], busy_ms=out[4])
+
+
 def profile_read(ctx: Context, stage: str):
     """(device ms, launches, algorithmic bytes) accumulated for one stage since profile_enable."""
     ms = C.c_double()
