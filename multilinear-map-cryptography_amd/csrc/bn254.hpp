@@ -155,53 +155,7 @@ TNS_HD Fp<C> dbl(const Fp<C> &a) {
 }
 
 #if defined(__HIPCC__)
-// Device: product-scanning (FIPS) Montgomery multiplication.  Column k accumulates every
-// a_i*b_j and m_i*M_j with i + j = k into a 64-bit register pair with v_mad_u64_u32, whose
-// carry-out (VCC) feeds a 32-bit overflow counter via v_addc_co_u32 -- 2 VALU ops per limb
-// product instead of the ~4.4 hipcc emits for the CIOS form (tools/mulbench.hip: 1.46x).
-#define TNS_MAC_VV(acc, c2, x, y)                                                               \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"          \
-               : "+v"(acc), "+v"(c2)                                                            \
-               : "v"(x), "v"(y)                                                                 \
-               : "vcc")
-#define TNS_MAC_VS(acc, c2, x, y)                                                               \
-  asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"          \
-               : "+v"(acc), "+v"(c2)                                                            \
-               : "v"(x), "s"(y)                                                                 \
-               : "vcc")
-template <class C>
-__device__ __forceinline__ Fp<C> mul_ps_dev(const Fp<C> &a, const Fp<C> &b) {
-  u32 m[8], r[8];
-  u64 acc = 0;
-  u32 c2 = 0;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-#pragma unroll
-    for (int i = 0; i <= k; i++) TNS_MAC_VV(acc, c2, a.v[i], b.v[k - i]);
-#pragma unroll
-    for (int i = 0; i < k; i++) TNS_MAC_VS(acc, c2, m[i], C::M[k - i]);
-    m[k] = (u32)acc * C::INV;
-    TNS_MAC_VS(acc, c2, m[k], C::M[0]);  // clears the low word
-    acc = (acc >> 32) | ((u64)c2 << 32);
-    c2 = 0;
-  }
-#pragma unroll
-  for (int k = 8; k < 15; k++) {
-#pragma unroll
-    for (int i = k - 7; i <= 7; i++) TNS_MAC_VV(acc, c2, a.v[i], b.v[k - i]);
-#pragma unroll
-    for (int i = k - 7; i <= 7; i++) TNS_MAC_VS(acc, c2, m[i], C::M[k - i]);
-    r[k - 8] = (u32)acc;
-    acc = (acc >> 32) | ((u64)c2 << 32);
-    c2 = 0;
-  }
-  r[7] = (u32)acc;  // < 2M < 2^256 by the no-carry bound
-  Fp<C> o;
-#pragma unroll
-  for (int i = 0; i < 8; i++) o.v[i] = r[i];
-  reduce_once(o);
-  return o;
-}
+#include "mont_mul.inc"
 #endif
 
 // Host (and reference): CIOS Montgomery product, no-carry variant (top modulus limb < 2^31 - 1).

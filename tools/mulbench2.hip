@@ -118,11 +118,16 @@ __device__ __forceinline__ Fp<C> mul_dual(const Fp<C> &a, const Fp<C> &b) {
   return o;
 }
 
+#include "mac_blocks.inc"
+
 template <int V>
 __device__ __forceinline__ Fq M(const Fq &a, const Fq &b) {
   if (V == 0) return mul(a, b);
   if (V == 1) return mul_sgpr(a, b);
-  return mul_dual(a, b);
+  if (V == 2) return mul_dual(a, b);
+  if (V == 3) return mul_blk2(a, b);
+  if (V == 4) return mul_blk4(a, b);
+  return mul_blk8(a, b);
 }
 
 // madd-2008-s with the variant multiply (no special cases: benchmark only)
@@ -172,6 +177,9 @@ __global__ void k_check(const Fq *x, int n, unsigned *bad) {
   Fq a = x[2 * i], b = x[2 * i + 1];
   Fq p = mul(a, b);
   if (!(mul_sgpr(a, b) == p) || !(mul_dual(a, b) == p)) atomicAdd(bad, 1u);
+  if (!(mul_blk2(a, b) == p)) atomicAdd(bad + 1, 1u);
+  if (!(mul_blk4(a, b) == p)) atomicAdd(bad + 2, 1u);
+  if (!(mul_blk8(a, b) == p)) atomicAdd(bad + 3, 1u);
 }
 
 static float time_ms(void (*launch)(void *), void *arg) {
@@ -225,17 +233,20 @@ int main() {
   hipMalloc(&d, sizeof(Fq) * 2 * n + 64);
   hipMemcpy(d, h.data(), sizeof(Fq) * 2 * n, hipMemcpyHostToDevice);
   unsigned *bad;
-  hipMalloc(&bad, 4);
-  hipMemset(bad, 0, 4);
+  hipMalloc(&bad, 16);
+  hipMemset(bad, 0, 16);
   k_check<<<(n + 255) / 256, 256>>>(d, (int)n, bad);
-  unsigned hb = 0;
-  hipMemcpy(&hb, bad, 4, hipMemcpyDeviceToHost);
-  printf("variant mismatches vs library mul: %u of %zu\n", hb, n);
+  unsigned hb[4] = {0, 0, 0, 0};
+  hipMemcpy(hb, bad, 16, hipMemcpyDeviceToHost);
+  printf("variant mismatches vs library mul: sgpr/dual %u, blk2 %u, blk4 %u, blk8 %u of %zu\n", hb[0], hb[1], hb[2],
+         hb[3], n);
 
   Args A{d, nullptr, blocks, 100, 0};
   const double muls = (double)n * A.iters;
   float t0 = time_ms(L_mul<0>, &A), t1 = time_ms(L_mul<1>, &A), t2 = time_ms(L_mul<2>, &A);
-  printf("mul chain   : vcc %.1f  sgpr %.1f  dual %.1f  G mul/s\n", muls / t0 / 1e6, muls / t1 / 1e6, muls / t2 / 1e6);
+  float t3 = time_ms(L_mul<3>, &A), t4 = time_ms(L_mul<4>, &A), t5 = time_ms(L_mul<5>, &A);
+  printf("mul chain   : vcc %.1f  sgpr %.1f  dual %.1f  blk2 %.1f  blk4 %.1f  blk8 %.1f  G mul/s\n", muls / t0 / 1e6,
+         muls / t1 / 1e6, muls / t2 / 1e6, muls / t3 / 1e6, muls / t4 / 1e6, muls / t5 / 1e6);
   A.iters = 2000;
   float tp = time_ms(L_peak, &A);
   printf("peak v_mad_u64_u32: %.2f T mad/s (independent streams)\n", (double)n * A.iters * 8 / tp / 1e9);
@@ -251,7 +262,8 @@ int main() {
   A = Args{accs, pts, blocks, 20, npts};
   const double madds = (double)n * A.iters;
   float m0 = time_ms(L_madd<0>, &A), m1 = time_ms(L_madd<1>, &A), m2 = time_ms(L_madd<2>, &A);
-  printf("madd        : vcc %.2f  sgpr %.2f  dual %.2f  G madd/s\n", madds / m0 / 1e6, madds / m1 / 1e6,
-         madds / m2 / 1e6);
+  float m3 = time_ms(L_madd<3>, &A), m4 = time_ms(L_madd<4>, &A), m5 = time_ms(L_madd<5>, &A);
+  printf("madd        : vcc %.2f  sgpr %.2f  dual %.2f  blk2 %.2f  blk4 %.2f  blk8 %.2f  G madd/s\n",
+         madds / m0 / 1e6, madds / m1 / 1e6, madds / m2 / 1e6, madds / m3 / 1e6, madds / m4 / 1e6, madds / m5 / 1e6);
   return 0;
 }
