@@ -211,6 +211,33 @@ int tns_shout_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *p
 int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, size_t n,
                    uint64_t out_proj[12]);
 
+/* ---------------------------------------------------------------- verifiers (host)
+ * CommitmentVerificationKey (src/utils.rs:64-75, :104-112): G1 generator, G2 generator and
+ * tau*G2, affine Montgomery limbs; G2 coordinates as x.c0, x.c1, y.c0, y.c1 (Fq2 = Fq[u]/(u^2+1)),
+ * identity = all zeros. */
+typedef struct tns_vk {
+  uint64_t g1[8];
+  uint64_t g2[16];
+  uint64_t g2_tau[16];
+} tns_vk;
+int tns_verifier_key(const tns_params *params, tns_vk *out);
+/* KZGCommitment::verify (src/commitments.rs:201-228): e(C - v G1, G2) == e(pi, tau G2 - z G2). */
+int tns_kzg_verify(const tns_vk *vk, const uint64_t commitment_proj[12], const uint64_t z[4],
+                   const uint64_t value[4], const uint64_t proof_proj[12], int *ok);
+/* KZGCommitment::batch_verify (src/commitments.rs:230-301), the reference's equation as written;
+ * arrays of n entries (commitments/proofs uint64_t[12] each, points/values uint64_t[4]). */
+int tns_kzg_batch_verify(const tns_vk *vk, size_t n, const uint64_t *commitments_proj, const uint64_t *points,
+                         const uint64_t *values, const uint64_t *proofs_proj, int *ok);
+/* Twist::verify / Shout::verify (src/twist.rs:255-304, src/shout.rs:225-274) on a proof of
+ * tns_twist_prove / tns_shout_prove; *ok = 1 valid, 0 invalid. */
+int tns_twist_verify(const tns_vk *vk, const tns_proof *proof, int *ok);
+int tns_shout_verify(const tns_vk *vk, const tns_proof *proof, int *ok);
+/* Bn254::pairing(P, Q) (arkworks optimal ate): 12 Fq (Montgomery), tower order
+ * c0.c0.c0, c0.c0.c1, c0.c1.c0, ..., c1.c2.c1.  Test / interop utility. */
+int tns_pairing(const uint64_t g1_affine[8], const uint64_t g2_affine[16], uint64_t out[48]);
+/* k * Q on G2 for a canonical scalar k (uint64_t[4]). */
+int tns_g2_mul(const uint64_t g2_affine[16], const uint64_t k_canonical[4], uint64_t out[16]);
+
 /* ---------------------------------------------------------------- one proof across GPUs
  * SURVEY 8(e) / BASELINE C5: the evaluation vectors and the SRS of ONE Twist/Shout proof
  * sharded over `size` ranks (one process -- or one tns_ctx -- per GPU).  Rank r holds the

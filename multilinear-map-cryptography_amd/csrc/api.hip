@@ -940,6 +940,125 @@ int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *
   });
 }
 
+// ---------------------------------------------------------------- verifiers (host)
+static G2Affine g2_from_limbs(const uint64_t in[16]) {
+  G2Affine g;
+  std::memcpy(&g.x0, in, 32);
+  std::memcpy(&g.x1, in + 4, 32);
+  std::memcpy(&g.y0, in + 8, 32);
+  std::memcpy(&g.y1, in + 12, 32);
+  g.inf = g.x0.is_zero() && g.x1.is_zero() && g.y0.is_zero() && g.y1.is_zero();
+  if (!g.inf && !g2_on_curve(g)) throw Error(TNS_ERR_INVALID_PARAMETERS, "G2 point not on the twist");
+  return g;
+}
+static void g2_to_limbs(const G2Affine &g, uint64_t out[16]) {
+  if (g.inf) {
+    std::memset(out, 0, 128);
+    return;
+  }
+  std::memcpy(out, &g.x0, 32);
+  std::memcpy(out + 4, &g.x1, 32);
+  std::memcpy(out + 8, &g.y0, 32);
+  std::memcpy(out + 12, &g.y1, 32);
+}
+static G1Affine g1_from_limbs(const uint64_t in[8]) {
+  G1Affine a;
+  std::memcpy(&a.x, in, 32);
+  std::memcpy(&a.y, in + 4, 32);
+  if (!a.is_inf() && !g1_on_curve(a)) throw Error(TNS_ERR_INVALID_PARAMETERS, "G1 point not on the curve");
+  return a;
+}
+struct Vk {
+  G1Affine g1;
+  G2Affine g2, g2_tau;
+};
+static Vk vk_load(const tns_vk *vk) { return Vk{g1_from_limbs(vk->g1), g2_from_limbs(vk->g2), g2_from_limbs(vk->g2_tau)}; }
+static Fr fr_load(const uint64_t x[4]) {
+  Fr r;
+  std::memcpy(&r, x, 32);
+  return r;
+}
+
+static int verify_proof(const tns_vk *vk, const tns_proof *p, const char *l0, const char *l1, int *ok) {
+  return guarded([&]() {
+    const Vk k = vk_load(vk);
+    if (p->num_rounds > TNS_MAX_ROUNDS || p->num_openings > 2) throw Error(TNS_ERR_INVALID_PARAMETERS, "malformed proof");
+    G1Affine C[2] = {proj_to_affine_host(p->commitments[0]), proj_to_affine_host(p->commitments[1])};
+    G1Affine pi[2] = {proj_to_affine_host(p->opening_proofs[0]), proj_to_affine_host(p->opening_proofs[1])};
+    Fr vals[2] = {fr_load(p->final_evaluations[0]), fr_load(p->final_evaluations[1])};
+    std::vector<Fr> rounds(4 * (size_t)(p->num_rounds ? p->num_rounds : 1));
+    std::memcpy(rounds.data(), p->round_polynomials, 128 * (size_t)p->num_rounds);
+    *ok = protocol_verify_host(k.g1, k.g2, k.g2_tau, l0, l1, C, rounds.data(), p->num_rounds,
+                               fr_load(p->final_evaluation), p->num_openings, pi, vals)
+              ? 1 : 0;
+    return TNS_OK;
+  });
+}
+
+int tns_verifier_key(const tns_params *params, tns_vk *out) {
+  return guarded([&]() {
+    G1Affine g1;
+    G2Affine g2, g2t;
+    verifier_key(fr_load(params->tau), &g1, &g2, &g2t);
+    std::memcpy(out->g1, &g1, 64);
+    g2_to_limbs(g2, out->g2);
+    g2_to_limbs(g2t, out->g2_tau);
+    return TNS_OK;
+  });
+}
+
+int tns_kzg_verify(const tns_vk *vk, const uint64_t commitment_proj[12], const uint64_t z[4], const uint64_t value[4],
+                   const uint64_t proof_proj[12], int *ok) {
+  return guarded([&]() {
+    const Vk k = vk_load(vk);
+    *ok = kzg_verify_host(k.g1, k.g2, k.g2_tau, proj_to_affine_host(commitment_proj), fr_load(z), fr_load(value),
+                          proj_to_affine_host(proof_proj))
+              ? 1 : 0;
+    return TNS_OK;
+  });
+}
+
+int tns_kzg_batch_verify(const tns_vk *vk, size_t n, const uint64_t *commitments_proj, const uint64_t *points,
+                         const uint64_t *values, const uint64_t *proofs_proj, int *ok) {
+  return guarded([&]() {
+    const Vk k = vk_load(vk);
+    std::vector<G1Affine> C(n), pi(n);
+    std::vector<Fr> z(n), v(n);
+    for (size_t i = 0; i < n; i++) {
+      C[i] = proj_to_affine_host(commitments_proj + 12 * i);
+      pi[i] = proj_to_affine_host(proofs_proj + 12 * i);
+      z[i] = fr_load(points + 4 * i);
+      v[i] = fr_load(values + 4 * i);
+    }
+    *ok = kzg_batch_verify_host(k.g1, k.g2, k.g2_tau, n, C.data(), z.data(), v.data(), pi.data()) ? 1 : 0;
+    return TNS_OK;
+  });
+}
+
+int tns_twist_verify(const tns_vk *vk, const tns_proof *proof, int *ok) {
+  return verify_proof(vk, proof, "address_commitment", "value_commitment", ok);
+}
+
+int tns_shout_verify(const tns_vk *vk, const tns_proof *proof, int *ok) {
+  return verify_proof(vk, proof, "table_commitment", "index_commitment", ok);
+}
+
+int tns_pairing(const uint64_t g1_affine[8], const uint64_t g2_affine[16], uint64_t out[48]) {
+  return guarded([&]() {
+    Fq e[12];
+    pairing_value(g1_from_limbs(g1_affine), g2_from_limbs(g2_affine), e);
+    std::memcpy(out, e, sizeof e);
+    return TNS_OK;
+  });
+}
+
+int tns_g2_mul(const uint64_t g2_affine[16], const uint64_t k[4], uint64_t out[16]) {
+  return guarded([&]() {
+    g2_to_limbs(g2_mul(g2_from_limbs(g2_affine), k), out);
+    return TNS_OK;
+  });
+}
+
 // ---------------------------------------------------------------- communicators
 int tns_comm_unique_id(uint8_t uid[128]) {
   return guarded([&]() {

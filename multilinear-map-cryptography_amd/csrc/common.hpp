@@ -355,6 +355,31 @@ void comm_unique_id(uint8_t out[128]);
 G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part);
 std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k);
 
+// pairing.cpp: BN254 G2 (D-type twist, affine over Fq2 = Fq[u]/(u^2+1)) and the pairing
+struct G2Affine {
+  Fq x0, x1, y0, y1;  // x = x0 + x1 u, y = y0 + y1 u
+  bool inf = false;
+};
+G2Affine g2_generator();
+G2Affine g2_add(const G2Affine &a, const G2Affine &b);
+G2Affine g2_neg(const G2Affine &a);
+G2Affine g2_mul(const G2Affine &a, const uint64_t k_canonical[4]);
+bool g2_on_curve(const G2Affine &a);
+bool pairing_eq(const G1Affine &P1, const G2Affine &Q1, const G1Affine &P2, const G2Affine &Q2);
+void pairing_value(const G1Affine &P, const G2Affine &Q, Fq out[12]);
+
+// verify.cpp: the reference verifiers (host)
+G1Xyzz g1_mul_host(const G1Xyzz &P, const Fr &k);
+void verifier_key(const Fr &tau, G1Affine *g1, G2Affine *g2, G2Affine *g2_tau);
+bool kzg_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine &g2_tau, const G1Affine &C,
+                     const Fr &z, const Fr &v, const G1Affine &pi);
+bool kzg_batch_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine &g2_tau, size_t n,
+                           const G1Affine *C, const Fr *z, const Fr *v, const G1Affine *pi);
+struct HostTranscript;
+bool protocol_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine &g2_tau, const char *label0,
+                          const char *label1, const G1Affine C[2], const Fr *rounds, unsigned nv,
+                          const Fr &final_eval, unsigned n_openings, const G1Affine pi[2], const Fr vals[2]);
+
 // host-side helpers (transcript.cpp)
 struct HostTranscript {
   std::vector<uint8_t> state;

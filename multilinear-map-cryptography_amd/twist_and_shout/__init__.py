@@ -253,11 +253,48 @@ class ProverParams:
 
 
 @dataclass
+class CommitmentVerificationKey:
+    """src/utils.rs:64-75: G1 generator, G2 generator, [tau]_2 (host-side pairing verifier)."""
+    raw: N.TnsVk = field(repr=False)
+
+    @staticmethod
+    def from_tau(tau: int) -> "CommitmentVerificationKey":
+        r = N.TnsParams()
+        r.tau = (C.c_uint64 * 4)(*to_mont([tau])[0])
+        vk = N.TnsVk()
+        _check(N.load().tns_verifier_key(C.byref(r), C.byref(vk)))
+        return CommitmentVerificationKey(vk)
+
+    @staticmethod
+    def _g2(limbs) -> Optional[Tuple[Tuple[int, int], Tuple[int, int]]]:
+        a = np.ctypeslib.as_array(limbs).reshape(4, 4)
+        if not a.any():
+            return None
+        v = from_mont(a, P_MOD)
+        return ((v[0], v[1]), (v[2], v[3]))
+
+    @property
+    def g1_generator(self) -> G1Affine:
+        a = np.ctypeslib.as_array(self.raw.g1).reshape(2, 4)
+        x, y = from_mont(a, P_MOD)
+        return (x, y)
+
+    @property
+    def g2_generator(self):
+        return self._g2(self.raw.g2)
+
+    @property
+    def g2_tau(self):
+        return self._g2(self.raw.g2_tau)
+
+
+@dataclass
 class VerifierParams:
-    """src/utils.rs:37-50 (commitment_vk / G2 elements: verifier side, out of scope)."""
+    """src/utils.rs:37-50"""
     log_size: int
     max_operations: int
     fiat_shamir_seed: bytes
+    commitment_vk: Optional[CommitmentVerificationKey] = None
 
 
 def setup_params(log_size: int, device: int = 0) -> Tuple[ProverParams, VerifierParams]:
@@ -270,7 +307,8 @@ def setup_params(log_size: int, device: int = 0) -> Tuple[ProverParams, Verifier
     seed = bytes(raw.fiat_shamir_seed)
     cp = CommitmentParams(Srs(ctx, h), tau)
     pp = ProverParams(int(raw.log_size), int(raw.max_operations), cp, seed, raw)
-    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed)
+    vk = CommitmentVerificationKey.from_tau(tau)
+    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed, vk)
 
 
 # ----------------------------------------------------------------------------- transcript
@@ -368,6 +406,31 @@ class KZGCommitment:
                                      N.p64(z), N.p64(v), N.p64(pi)))
         return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
 
+
+    @staticmethod
+    def verify(vk: "CommitmentVerificationKey", commitment: KZGCommitmentValue, point: int, value: int,
+               proof: KZGProof) -> bool:
+        """src/commitments.rs:201-228: e(C - [v]_1, [1]_2) == e(pi, [tau]_2 - [z]_2)."""
+        ok = C.c_int()
+        _check(N.load().tns_kzg_verify(C.byref(vk.raw), N.p64(_affine_to_proj(commitment.commitment)),
+                                       N.p64(to_mont([point])[0]), N.p64(to_mont([value])[0]),
+                                       N.p64(_affine_to_proj(proof.proof)), C.byref(ok)))
+        return bool(ok.value)
+
+    @staticmethod
+    def batch_verify(vk: "CommitmentVerificationKey", commitments, points, values, proofs) -> bool:
+        """src/commitments.rs:230-301 (the reference's batched equation, as written)."""
+        if not (len(commitments) == len(points) == len(values) == len(proofs)):
+            raise CommitmentError("Batch verify input lengths must match")
+        n = len(commitments)
+        if n == 0:
+            return True
+        cs = np.concatenate([_affine_to_proj(c.commitment) for c in commitments])
+        ps = np.concatenate([_affine_to_proj(p.proof) for p in proofs])
+        ok = C.c_int()
+        _check(N.load().tns_kzg_batch_verify(C.byref(vk.raw), n, N.p64(cs), N.p64(to_mont(list(points))),
+                                             N.p64(to_mont(list(values))), N.p64(ps), C.byref(ok)))
+        return bool(ok.value)
 
     @staticmethod
     def commit_evaluations(params: CommitmentParams, evaluations) -> KZGCommitmentValue:
@@ -596,6 +659,25 @@ class TwistProof:
     final_mle_evals: List[int] = field(default_factory=list)
 
 
+def _pack_proof(commitments, rounds, final_eval, openings, finals) -> N.TnsProof:
+    """Proof fields (affine points / ints) -> the C proof struct (for the verifiers)."""
+    pr = N.TnsProof()
+    for i, c in enumerate(commitments):
+        pr.commitments[i] = (C.c_uint64 * 12)(*_affine_to_proj(c))
+    pr.num_rounds = len(rounds)
+    for r, coeffs in enumerate(rounds):
+        m = to_mont(list(coeffs))
+        for x in range(4):
+            pr.round_polynomials[r][x] = (C.c_uint64 * 4)(*m[x])
+    pr.final_evaluation = (C.c_uint64 * 4)(*to_mont([final_eval])[0])
+    pr.num_openings = len(openings)
+    for i, o in enumerate(openings):
+        pr.opening_proofs[i] = (C.c_uint64 * 12)(*_affine_to_proj(o))
+    for i, v in enumerate(finals):
+        pr.final_evaluations[i] = (C.c_uint64 * 4)(*to_mont([v])[0])
+    return pr
+
+
 def _unpack_proof(pr: N.TnsProof, n_mles: int):
     nr = pr.num_rounds
     rounds = np.ctypeslib.as_array(pr.round_polynomials)[:nr]
@@ -637,6 +719,16 @@ class Twist:
 
     def prove(self, trace: MemoryTrace) -> TwistProof:
         return self.prove_soa(*trace.soa())
+
+    @staticmethod
+    def verify(proof: TwistProof, verifier_params: VerifierParams) -> bool:
+        """src/twist.rs:255-304 (host: sum-check replay + two pairing checks)."""
+        pr = _pack_proof([proof.address_commitment.commitment, proof.value_commitment.commitment],
+                         proof.consistency_proof.round_polynomials, proof.consistency_proof.final_evaluation,
+                         [p.proof for p in proof.opening_proofs], proof.final_evaluations)
+        ok = C.c_int()
+        _check(N.load().tns_twist_verify(C.byref(verifier_params.commitment_vk.raw), C.byref(pr), C.byref(ok)))
+        return bool(ok.value)
 
     def prove_sharded(self, comm: "Comm", addr: np.ndarray, value: np.ndarray, is_write: np.ndarray,
                       n_total: int) -> TwistProof:
@@ -715,6 +807,16 @@ class Shout:
         di = _nonempty_buf(ctx, indices, np.uint64)
         return shout_proof_from_raw(shout_prove_sharded_resident(self.prover_params, comm, de, len(e),
                                                                  n_entries_total, di, len(indices), n_lookups_total))
+
+    @staticmethod
+    def verify(proof: ShoutProof, verifier_params: VerifierParams) -> bool:
+        """src/shout.rs:225-274"""
+        pr = _pack_proof([proof.table_commitment.commitment, proof.index_commitment.commitment],
+                         proof.lookup_proof.round_polynomials, proof.lookup_proof.final_evaluation,
+                         [p.proof for p in proof.opening_proofs], proof.final_evaluations)
+        ok = C.c_int()
+        _check(N.load().tns_shout_verify(C.byref(verifier_params.commitment_vk.raw), C.byref(pr), C.byref(ok)))
+        return bool(ok.value)
 
     def prove(self, table: LookupTable) -> ShoutProof:
         e = to_mont(table.entries) if table.entries else np.zeros((0, 4), dtype=np.uint64)
@@ -851,7 +953,8 @@ def setup_params_shard(log_size: int, rank: int, size: int, device: int = 0,
     seed = bytes(raw.fiat_shamir_seed)
     cp = CommitmentParams(Srs(ctx, h), tau)
     pp = ProverParams(int(raw.log_size), int(raw.max_operations), cp, seed, raw)
-    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed)
+    vk = CommitmentVerificationKey.from_tau(tau)
+    return pp, VerifierParams(int(raw.log_size), int(raw.max_operations), seed, vk)
 
 
 def shard_slice(n_total: int, rank: int, size: int) -> Tuple[int, int]:
@@ -907,6 +1010,32 @@ def bench_trace_slice(memory_size: int, n_total: int, first: int, count: int):
         _check(N.load().tns_bench_trace_slice(memory_size, n_total, first, count, N.p64(addr), N.p64(val),
                                               N.p8(isw)))
     return addr, fr_from_u64_array(val), isw
+
+
+def pairing(P: G1Affine, Q) -> List[int]:
+    """Bn254::pairing(P, Q) -- 12 Fq coefficients (canonical) in the product's tower order."""
+    g1 = np.zeros(8, dtype=np.uint64)
+    if P is not None:
+        g1[:4] = to_mont([P[0]], P_MOD)[0]
+        g1[4:] = to_mont([P[1]], P_MOD)[0]
+    g2 = np.zeros(16, dtype=np.uint64)
+    if Q is not None:
+        g2[:] = to_mont([Q[0][0], Q[0][1], Q[1][0], Q[1][1]], P_MOD).reshape(-1)
+    out = np.zeros(48, dtype=np.uint64)
+    _check(N.load().tns_pairing(N.p64(g1), N.p64(g2), N.p64(out)))
+    return from_mont(out.reshape(12, 4), P_MOD)
+
+
+def g2_mul(Q, k: int):
+    g2 = np.zeros(16, dtype=np.uint64)
+    g2[:] = to_mont([Q[0][0], Q[0][1], Q[1][0], Q[1][1]], P_MOD).reshape(-1)
+    kk = np.array([(k % R_MOD >> (64 * i)) & ((1 << 64) - 1) for i in range(4)], dtype=np.uint64)
+    out = np.zeros(16, dtype=np.uint64)
+    _check(N.load().tns_g2_mul(N.p64(g2), N.p64(kk), N.p64(out)))
+    if not out.any():
+        return None
+    v = from_mont(out.reshape(4, 4), P_MOD)
+    return ((v[0], v[1]), (v[2], v[3]))
 
 
 def profile_enable(ctx: Context, on: bool = True):

@@ -63,6 +63,10 @@ class TnsTerm(C.Structure):
 
 
 # (name, restype, argtypes) for every symbol of include/tns.h
+class TnsVk(C.Structure):
+    _fields_ = [("g1", C.c_uint64 * 8), ("g2", C.c_uint64 * 16), ("g2_tau", C.c_uint64 * 16)]
+
+
 SIGNATURES = [
     ("tns_last_error", C.c_char_p, []),
     ("tns_version", C.c_int, []),
@@ -120,6 +124,13 @@ SIGNATURES = [
     ("tns_fr_to_canonical", None, [U64P, C.c_size_t, U64P]),
     ("tns_fq_to_canonical", None, [U64P, C.c_size_t, U64P]),
     ("tns_bench_trace", C.c_int, [C.c_size_t, C.c_size_t, U64P, U64P, U8P]),
+    ("tns_verifier_key", C.c_int, [C.POINTER(TnsParams), C.POINTER(TnsVk)]),
+    ("tns_kzg_verify", C.c_int, [C.POINTER(TnsVk), U64P, U64P, U64P, U64P, C.POINTER(C.c_int)]),
+    ("tns_kzg_batch_verify", C.c_int, [C.POINTER(TnsVk), C.c_size_t, U64P, U64P, U64P, U64P, C.POINTER(C.c_int)]),
+    ("tns_twist_verify", C.c_int, [C.POINTER(TnsVk), C.POINTER(TnsProof), C.POINTER(C.c_int)]),
+    ("tns_shout_verify", C.c_int, [C.POINTER(TnsVk), C.POINTER(TnsProof), C.POINTER(C.c_int)]),
+    ("tns_pairing", C.c_int, [U64P, U64P, U64P]),
+    ("tns_g2_mul", C.c_int, [U64P, U64P, U64P]),
     ("tns_bench_trace_slice", C.c_int, [C.c_size_t, C.c_uint64, C.c_uint64, C.c_size_t, U64P, U64P, U8P]),
     ("tns_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("tns_comm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),

@@ -731,3 +731,215 @@ def barycentric_eval(ys, z: int) -> int:
                 w = R_MOD - w
             acc = (acc + ys[i] * w % R_MOD * di_inv) % R_MOD
     return acc * M % R_MOD
+
+
+# ----------------------------------------------------------------------------
+# BN254 pairing and the verifiers (src/commitments.rs:201-301, src/sumcheck.rs:113-150,
+# src/twist.rs:255-304, src/shout.rs:225-274; arkworks Bn254::pairing).  Restated in a
+# different representation from the product (csrc/pairing.cpp uses the Fq2/Fq6/Fq12 tower):
+# Fq12 = Fq[w] / (w^12 - 18 w^6 + 82), with u = w^6 - 9 (so u^2 = -1) and G2 on the D-type
+# twist y^2 = x^3 + 3/(9+u), untwisted by (x, y) -> (x w^2, y w^3).  The reduced optimal ate
+# pairing f_{6x+2,Q}(P) l_{T,pi Q}(P) l_{T+pi Q,-pi^2 Q}(P) ^ ((p^12-1)/r) is unique.
+# ----------------------------------------------------------------------------
+BN_X = 4965661367192848881
+G2_GEN = ((10857046999023057135944570762232829481370756359578518086990519993285655852781,
+           11559732032986387107991004021392285783925812861821192530917403151452391805634),
+          (8495653923123431417604973247489272438418190587263600148770280649306958101930,
+           4082367875863433681332203403145435568316851327593401208105741076214120093531))
+
+
+def _f12_mul(a, b):
+    p = P_MOD
+    t = [0] * 23
+    for i, x in enumerate(a):
+        if x:
+            for j, y in enumerate(b):
+                t[i + j] += x * y
+    for k in range(22, 11, -1):  # w^12 = 18 w^6 - 82
+        c = t[k]
+        if c:
+            t[k - 6] += 18 * c
+            t[k - 12] -= 82 * c
+    return [x % p for x in t[:12]]
+
+
+def _f12_one():
+    return [1] + [0] * 11
+
+
+def _f12_pow(a, e):
+    r = _f12_one()
+    for bit in bin(e)[2:]:
+        r = _f12_mul(r, r)
+        if bit == "1":
+            r = _f12_mul(r, a)
+    return r
+
+
+def _f12_inv(a):
+    # a^(p^12 - 2) (Fermat in the field Fq12)
+    return _f12_pow(a, P_MOD ** 12 - 2)
+
+
+def _f12_from_fq2(a, shift):
+    """(a0 + a1 u) * w^shift with u = w^6 - 9."""
+    r = [0] * 12
+    r[shift % 12] = (a[0] - 9 * a[1]) % P_MOD
+    r[(shift + 6) % 12] = a[1] % P_MOD
+    return r
+
+
+def _untwist(Q):
+    return (_f12_from_fq2(Q[0], 2), _f12_from_fq2(Q[1], 3))
+
+
+def _f12_add(a, b):
+    return [(x + y) % P_MOD for x, y in zip(a, b)]
+
+
+def _f12_sub(a, b):
+    return [(x - y) % P_MOD for x, y in zip(a, b)]
+
+
+def _line(T, S, P, tangent):
+    if tangent:
+        x2 = _f12_mul(T[0], T[0])
+        lam = _f12_mul([3 * v % P_MOD for v in x2], _f12_inv([2 * v % P_MOD for v in T[1]]))
+    else:
+        lam = _f12_mul(_f12_sub(S[1], T[1]), _f12_inv(_f12_sub(S[0], T[0])))
+    l = _f12_sub(_f12_sub(P[1], T[1]), _f12_mul(lam, _f12_sub(P[0], T[0])))
+    x3 = _f12_sub(_f12_sub(_f12_mul(lam, lam), T[0]), S[0])
+    y3 = _f12_sub(_f12_mul(lam, _f12_sub(T[0], x3)), T[1])
+    return l, (x3, y3)
+
+
+def pairing(P, Q):
+    """Reduced optimal ate pairing e(P, Q) (flat Fq12 coefficient list); P affine G1 or None,
+    Q = ((x0, x1), (y0, y1)) on the twist or None."""
+    if P is None or Q is None:
+        return _f12_one()
+    q = _untwist(Q)
+    Pf = ([P[0] % P_MOD] + [0] * 11, [P[1] % P_MOD] + [0] * 11)
+    f, T = _f12_one(), q
+    for bit in bin(6 * BN_X + 2)[3:]:
+        l, T = _line(T, T, Pf, True)
+        f = _f12_mul(_f12_mul(f, f), l)
+        if bit == "1":
+            l, T = _line(T, q, Pf, False)
+            f = _f12_mul(f, l)
+    q1 = (_f12_pow(q[0], P_MOD), _f12_pow(q[1], P_MOD))
+    q2 = (_f12_pow(q1[0], P_MOD), [(-v) % P_MOD for v in _f12_pow(q1[1], P_MOD)])
+    l, T = _line(T, q1, Pf, False)
+    f = _f12_mul(f, l)
+    l, T = _line(T, q2, Pf, False)
+    f = _f12_mul(f, l)
+    return _f12_pow(f, (P_MOD ** 12 - 1) // R_MOD)
+
+
+def tower_to_flat(c):
+    """Product layout (12 Fq: c0.c0.c0, c0.c0.c1, ..., c1.c2.c1 of Fq12 = Fq6[w]/(w^2 - v),
+    Fq6 = Fq2[v]/(v^3 - xi)) -> flat coefficients in w (v = w^2, u = w^6 - 9)."""
+    r = [0] * 12
+    for i in range(2):          # w^i
+        for j in range(3):      # v^j = w^(2j)
+            a0, a1 = c[6 * i + 2 * j], c[6 * i + 2 * j + 1]
+            for k, v in enumerate(_f12_from_fq2((a0, a1), i + 2 * j)):
+                r[k] = (r[k] + v) % P_MOD
+    return r
+
+
+# G2 arithmetic on the twist (Fq2 pairs), for the verifying key and batch verification
+def _f2_mul(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P_MOD, (a[0] * b[1] + a[1] * b[0]) % P_MOD)
+
+
+def _f2_inv(a):
+    n = pow((a[0] * a[0] + a[1] * a[1]) % P_MOD, P_MOD - 2, P_MOD)
+    return (a[0] * n % P_MOD, (-a[1]) * n % P_MOD)
+
+
+def g2_add(A, B):
+    if A is None:
+        return B
+    if B is None:
+        return A
+    if A[0] == B[0]:
+        if A[1] != B[1] or A[1] == (0, 0):
+            return None
+        x2 = _f2_mul(A[0], A[0])
+        lam = _f2_mul(((3 * x2[0]) % P_MOD, (3 * x2[1]) % P_MOD), _f2_inv(((2 * A[1][0]) % P_MOD, (2 * A[1][1]) % P_MOD)))
+    else:
+        lam = _f2_mul(((B[1][0] - A[1][0]) % P_MOD, (B[1][1] - A[1][1]) % P_MOD),
+                      _f2_inv(((B[0][0] - A[0][0]) % P_MOD, (B[0][1] - A[0][1]) % P_MOD)))
+    l2 = _f2_mul(lam, lam)
+    x3 = ((l2[0] - A[0][0] - B[0][0]) % P_MOD, (l2[1] - A[0][1] - B[0][1]) % P_MOD)
+    t = _f2_mul(lam, ((A[0][0] - x3[0]) % P_MOD, (A[0][1] - x3[1]) % P_MOD))
+    return (x3, ((t[0] - A[1][0]) % P_MOD, (t[1] - A[1][1]) % P_MOD))
+
+
+def g2_neg(A):
+    return None if A is None else (A[0], ((-A[1][0]) % P_MOD, (-A[1][1]) % P_MOD))
+
+
+def g2_mul(A, k):
+    r = None
+    for bit in bin(k % R_MOD)[2:] if k % R_MOD else "":
+        r = g2_add(r, r)
+        if bit == "1":
+            r = g2_add(r, A)
+    return r
+
+
+def verifier_key(params):
+    """CommitmentVerificationKey (src/utils.rs:104-112): (G1, G2, tau G2)."""
+    return dict(g1=G1_GEN, g2=G2_GEN, g2_tau=g2_mul(G2_GEN, params["tau"]))
+
+
+def kzg_verify(vk, C, z, v, proof):  # src/commitments.rs:201-228
+    left = affine_add(C, g1_neg(affine_mul(vk["g1"], v))) if C is not None else g1_neg(affine_mul(vk["g1"], v))
+    right = g2_add(vk["g2_tau"], g2_neg(g2_mul(vk["g2"], z)))
+    return pairing(left, vk["g2"]) == pairing(proof, right)
+
+
+def kzg_batch_verify(vk, Cs, zs, vs, proofs):  # src/commitments.rs:230-301, as written
+    if not (len(Cs) == len(zs) == len(vs) == len(proofs)):
+        raise ValueError("Batch verify input lengths must match")
+    if not Cs:
+        return True
+    rng = ChaCha20Rng(bytes([42] * 32))
+    gam = [fr_rand(rng) for _ in Cs]
+    bc = bp = bg2 = None
+    bv = 0
+    for C, z, v, pi, g in zip(Cs, zs, vs, proofs, gam):
+        bc = affine_add(bc, affine_mul(C, g)) if bc is not None else affine_mul(C, g)
+        bv = (bv + v * g) % R_MOD
+        bp = affine_add(bp, affine_mul(pi, g)) if bp is not None else affine_mul(pi, g)
+        bg2 = g2_add(bg2, g2_mul(g2_add(vk["g2_tau"], g2_neg(g2_mul(vk["g2"], z))), g))
+    left = affine_add(bc, g1_neg(affine_mul(vk["g1"], bv))) if bc is not None else g1_neg(affine_mul(vk["g1"], bv))
+    return pairing(left, vk["g2"]) == pairing(bp, bg2)
+
+
+def sumcheck_verify(rounds, final_eval, transcript):  # src/sumcheck.rs:113-150 (claimed 0)
+    cur = 0
+    for r, c in enumerate(rounds):
+        if (horner_eval(c, 0) + horner_eval(c, 1)) % R_MOD != cur:
+            return False
+        transcript.append_field_elements(f"sumcheck_round_{r}".encode(), c)
+        ch = transcript.challenge_field_element(f"sumcheck_challenge_{r}".encode())
+        cur = horner_eval(c, ch)
+    return cur == final_eval % R_MOD
+
+
+def protocol_verify(vk, seed, labels, C, rounds, final_eval, openings, values):
+    """Twist::verify (labels address/value) / Shout::verify (labels table/index)."""
+    tr = Transcript(seed)
+    tr.append_field_element(labels[0], commitment_hash(C[0]))
+    tr.append_field_element(labels[1], commitment_hash(C[1]))
+    if not sumcheck_verify(rounds, final_eval, tr):
+        return False
+    z = tr.challenge_field_elements(b"opening_challenges", len(rounds))
+    if z and len(openings) >= 2 and len(values) >= 2:
+        for k in range(2):
+            if not kzg_verify(vk, C[k], z[0], values[k], openings[k]):
+                return False
+    return True

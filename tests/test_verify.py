@@ -1,0 +1,148 @@
+"""Verifier path: BN254 pairing, KZG verify / batch_verify, SumCheck /
+Twist / Shout verify -- host code in libtns (csrc/pairing.cpp, csrc/verify.cpp), CPU-only.
+
+Pinned by (i) an independent restatement in the oracle (flat Fq12 = Fq[w]/(w^12 - 18w^6 + 82)
+against the product's Fq2/Fq6/Fq12 tower, compared coefficient by coefficient after a basis
+change), (ii) bilinearity / order / non-degeneracy, (iii) the reference's own verify tests:
+every golden proof (the reference's test traces, the demo, the C1 benchmark trace) verifies,
+and tampered proofs do not.  batch_verify is restated exactly as the reference writes it.
+"""
+import numpy as np
+import pytest
+
+from oracle import pyoracle as po
+
+import twist_and_shout as ts
+
+R, P = po.R_MOD, po.P_MOD
+
+
+def h(x):
+    return int(x, 16)
+
+
+def g1h(Pt):
+    return None if Pt is None else (h(Pt[0]), h(Pt[1]))
+
+
+@pytest.fixture(scope="module")
+def vk():
+    tau = po.setup_params(1, with_srs=False)["tau"]
+    return ts.CommitmentVerificationKey.from_tau(tau), tau
+
+
+def test_g2_generator_and_tau_key(vk):
+    key, tau = vk
+    assert key.g1_generator == po.G1_GEN
+    assert key.g2_generator == po.G2_GEN
+    assert key.g2_tau == po.g2_mul(po.G2_GEN, tau)
+
+
+@pytest.mark.parametrize("a,b", [(1, 1), (3, 7)])
+def test_pairing_matches_oracle(a, b):
+    Pa, Qb = po.affine_mul(po.G1_GEN, a), po.g2_mul(po.G2_GEN, b)
+    got = po.tower_to_flat(ts.pairing(Pa, Qb))
+    assert got == po.pairing(Pa, Qb)
+
+
+def test_pairing_bilinear_nondegenerate_order_r():
+    a, b = 0x1234567890ABCDEF, 0xFEDCBA0987654321
+    e_ab = ts.pairing(po.affine_mul(po.G1_GEN, a), ts.g2_mul(po.G2_GEN, b))
+    e_1 = ts.pairing(po.affine_mul(po.G1_GEN, a * b % R), po.G2_GEN)
+    assert e_ab == e_1
+    flat = po.tower_to_flat(ts.pairing(po.G1_GEN, po.G2_GEN))
+    assert flat != po._f12_one()
+    assert po._f12_pow(flat, R) == po._f12_one()
+    assert ts.pairing(None, po.G2_GEN) == [1] + [0] * 11
+
+
+def _twist_proof(case):
+    pr = case["proof"]
+    return ts.TwistProof(
+        ts.KZGCommitmentValue(g1h(pr["address_commitment"])), ts.KZGCommitmentValue(g1h(pr["value_commitment"])),
+        ts.SumCheckProof([[h(c) for c in r] for r in pr["round_polynomials"]], h(pr["final_evaluation"])),
+        [ts.KZGProof(g1h(p)) for p in pr["opening_proofs"]], [h(v) for v in pr["final_evaluations"]],
+        None if pr["opening_point"] is None else h(pr["opening_point"]))
+
+
+def _shout_proof(case):
+    pr = case["proof"]
+    return ts.ShoutProof(
+        ts.KZGCommitmentValue(g1h(pr["table_commitment"])), ts.KZGCommitmentValue(g1h(pr["index_commitment"])),
+        ts.SumCheckProof([[h(c) for c in r] for r in pr["round_polynomials"]], h(pr["final_evaluation"])),
+        [ts.KZGProof(g1h(p)) for p in pr["opening_proofs"]], [h(v) for v in pr["final_evaluations"]],
+        None if pr["opening_point"] is None else h(pr["opening_point"]))
+
+
+def _vp(vk):
+    return ts.VerifierParams(0, 0, bytes(32), vk[0])
+
+
+def test_twist_golden_proofs_verify(golden, vk):
+    for name, case in golden["twist"].items():
+        assert ts.Twist.verify(_twist_proof(case), _vp(vk)), name
+
+
+def test_shout_golden_proofs_verify(golden, vk):
+    for name, case in golden["shout"].items():
+        assert ts.Shout.verify(_shout_proof(case), _vp(vk)), name
+
+
+def test_tampered_proofs_do_not_verify(golden, vk):
+    case = golden["twist"]["demo_L3"]
+    good = _twist_proof(case)
+    bad = _twist_proof(case)
+    bad.final_evaluations[0] = (bad.final_evaluations[0] + 1) % R  # wrong opened value
+    assert not ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.consistency_proof.round_polynomials[0][0] = 1  # g(0) + g(1) != 0
+    assert not ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.opening_proofs[1] = ts.KZGProof(po.affine_mul(po.G1_GEN, 5))  # wrong quotient commitment
+    assert not ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.value_commitment = ts.KZGCommitmentValue(po.affine_mul(po.G1_GEN, 7))  # transcript and pairing
+    assert not ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.consistency_proof.final_evaluation = 3  # the last sum-check claim
+    assert not ts.Twist.verify(bad, _vp(vk))
+    assert ts.Twist.verify(good, _vp(vk))
+
+
+def test_kzg_verify_matches_oracle(golden, vk):
+    key, tau = vk
+    pr = golden["twist"]["demo_L3"]["proof"]
+    C, z = g1h(pr["address_commitment"]), h(pr["opening_point"])
+    v, pi = h(pr["final_evaluations"][0]), g1h(pr["opening_proofs"][0])
+    assert ts.KZGCommitment.verify(key, ts.KZGCommitmentValue(C), z, v, ts.KZGProof(pi))
+    assert not ts.KZGCommitment.verify(key, ts.KZGCommitmentValue(C), z, (v + 1) % R, ts.KZGProof(pi))
+    ovk = po.verifier_key({"tau": tau})
+    assert po.kzg_verify(ovk, C, z, v, pi)
+    assert not po.kzg_verify(ovk, C, z, (v + 1) % R, pi)
+
+
+def test_batch_verify_matches_oracle(golden, vk):
+    key, tau = vk
+    pr = golden["twist"]["demo_L3"]["proof"]
+    Cs = [g1h(pr["address_commitment"]), g1h(pr["value_commitment"])]
+    zs = [h(pr["opening_point"])] * 2
+    vs = [h(v) for v in pr["final_evaluations"]]
+    pis = [g1h(p) for p in pr["opening_proofs"]]
+    ovk = po.verifier_key({"tau": tau})
+    for n in (1, 2):
+        got = ts.KZGCommitment.batch_verify(key, [ts.KZGCommitmentValue(c) for c in Cs[:n]], zs[:n], vs[:n],
+                                            [ts.KZGProof(p) for p in pis[:n]])
+        assert got == po.kzg_batch_verify(ovk, Cs[:n], zs[:n], vs[:n], pis[:n])
+    assert ts.KZGCommitment.batch_verify(key, [], [], [], [])
+    with pytest.raises(ts.CommitmentError):
+        ts.KZGCommitment.batch_verify(key, [ts.KZGCommitmentValue(Cs[0])], [], [], [])
+
+
+def test_protocol_verify_matches_oracle(golden, vk):
+    key, tau = vk
+    ovk = po.verifier_key({"tau": tau})
+    case = golden["twist"]["small_trace_L3"]["proof"]
+    args = ([g1h(case["address_commitment"]), g1h(case["value_commitment"])],
+            [[h(c) for c in r] for r in case["round_polynomials"]], h(case["final_evaluation"]),
+            [g1h(p) for p in case["opening_proofs"]], [h(v) for v in case["final_evaluations"]])
+    assert po.protocol_verify(ovk, bytes(32), (b"address_commitment", b"value_commitment"), *args)
