@@ -238,6 +238,17 @@ int tns_pairing(const uint64_t g1_affine[8], const uint64_t g2_affine[16], uint6
 /* k * Q on G2 for a canonical scalar k (uint64_t[4]). */
 int tns_g2_mul(const uint64_t g2_affine[16], const uint64_t k_canonical[4], uint64_t out[16]);
 
+/* ---------------------------------------------------------------- wire format
+ * CanonicalSerialize of KZGCommitmentValue / KZGProof (src/commitments.rs:94-154) = the G1
+ * point's ark-serialize 0.4 encoding: 32 bytes (compressed: x LE, flags 0x80 y-negative /
+ * 0x40 infinity in the last byte) or 64 bytes (x, y).  Fr: 32 bytes LE.  Proofs
+ * (TwistProof / ShoutProof, src/twist.rs:76-89, src/shout.rs:64-79): fields in order, Vec as
+ * u64 LE length + elements.  Deserialisation validates (field range, curve membership). */
+int tns_g1_serialize(const uint64_t proj[12], int compressed, uint8_t *out);
+int tns_g1_deserialize(const uint8_t *in, int compressed, uint64_t proj_out[12]);
+int tns_proof_serialize(const tns_proof *proof, int compressed, uint8_t *out, size_t cap, size_t *len);
+int tns_proof_deserialize(const uint8_t *in, size_t len, int compressed, tns_proof *out);
+
 /* ---------------------------------------------------------------- one proof across GPUs
  * SURVEY 8(e) / BASELINE C5: the evaluation vectors and the SRS of ONE Twist/Shout proof
  * sharded over `size` ranks (one process -- or one tns_ctx -- per GPU).  Rank r holds the

@@ -1059,6 +1059,121 @@ int tns_g2_mul(const uint64_t g2_affine[16], const uint64_t k[4], uint64_t out[1
   });
 }
 
+// ---------------------------------------------------------------- wire format (host)
+int tns_g1_serialize(const uint64_t proj[12], int compressed, uint8_t *out) {
+  return guarded([&]() {
+    g1_serialize(proj_to_affine_host(proj), compressed != 0, out);
+    return TNS_OK;
+  });
+}
+
+int tns_g1_deserialize(const uint8_t *in, int compressed, uint64_t proj_out[12]) {
+  return guarded([&]() {
+    store_proj(g1_deserialize(in, compressed != 0, true), proj_out);
+    return TNS_OK;
+  });
+}
+
+namespace {
+struct Writer {
+  uint8_t *out;
+  size_t cap, n = 0;
+  void bytes(const uint8_t *p, size_t k) {
+    if (out && n + k <= cap) std::memcpy(out + n, p, k);
+    n += k;
+  }
+  void u64(uint64_t v) {
+    uint8_t b[8];
+    for (int i = 0; i < 8; i++) b[i] = (uint8_t)(v >> (8 * i));
+    bytes(b, 8);
+  }
+};
+struct Reader {
+  const uint8_t *in;
+  size_t len, n = 0;
+  const uint8_t *take(size_t k) {
+    if (n + k > len) throw Error(TNS_ERR_INVALID_PARAMETERS, "truncated proof bytes");
+    const uint8_t *p = in + n;
+    n += k;
+    return p;
+  }
+  uint64_t u64() {
+    const uint8_t *b = take(8);
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)b[i] << (8 * i);
+    return v;
+  }
+};
+}  // namespace
+
+int tns_proof_serialize(const tns_proof *p, int compressed, uint8_t *out, size_t cap, size_t *len) {
+  return guarded([&]() {
+    const size_t gs = compressed ? 32 : 64;
+    Writer w{out, cap};
+    uint8_t g[64], f[32];
+    for (int i = 0; i < 2; i++) {
+      g1_serialize(proj_to_affine_host(p->commitments[i]), compressed != 0, g);
+      w.bytes(g, gs);
+    }
+    w.u64(p->num_rounds);
+    for (uint32_t r = 0; r < p->num_rounds; r++) {
+      w.u64(4);
+      for (int x = 0; x < 4; x++) {
+        fr_serialize(fr_load(p->round_polynomials[r][x]), f);
+        w.bytes(f, 32);
+      }
+    }
+    fr_serialize(fr_load(p->final_evaluation), f);
+    w.bytes(f, 32);
+    w.u64(p->num_openings);
+    for (uint32_t i = 0; i < p->num_openings; i++) {
+      g1_serialize(proj_to_affine_host(p->opening_proofs[i]), compressed != 0, g);
+      w.bytes(g, gs);
+    }
+    w.u64(p->num_openings);  // final_evaluations has one value per opening
+    for (uint32_t i = 0; i < p->num_openings; i++) {
+      fr_serialize(fr_load(p->final_evaluations[i]), f);
+      w.bytes(f, 32);
+    }
+    *len = w.n;
+    if (out && w.n > cap) throw Error(TNS_ERR_INVALID_PARAMETERS, "output buffer too small");
+    return TNS_OK;
+  });
+}
+
+int tns_proof_deserialize(const uint8_t *in, size_t len, int compressed, tns_proof *p) {
+  return guarded([&]() {
+    std::memset(p, 0, sizeof *p);
+    const size_t gs = compressed ? 32 : 64;
+    Reader r{in, len};
+    for (int i = 0; i < 2; i++) store_proj(g1_deserialize(r.take(gs), compressed != 0, true), p->commitments[i]);
+    const uint64_t nr = r.u64();
+    if (nr > TNS_MAX_ROUNDS) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many sum-check rounds");
+    p->num_rounds = (uint32_t)nr;
+    for (uint64_t k = 0; k < nr; k++) {
+      if (r.u64() != 4) throw Error(TNS_ERR_INVALID_PARAMETERS, "round polynomial must have 4 coefficients");
+      for (int x = 0; x < 4; x++) {
+        const Fr v = fr_deserialize(r.take(32));
+        std::memcpy(p->round_polynomials[k][x], &v, 32);
+      }
+    }
+    const Fr fe = fr_deserialize(r.take(32));
+    std::memcpy(p->final_evaluation, &fe, 32);
+    const uint64_t no = r.u64();
+    if (no > 2) throw Error(TNS_ERR_INVALID_PARAMETERS, "more than two opening proofs");
+    p->num_openings = (uint32_t)no;
+    for (uint64_t i = 0; i < no; i++) store_proj(g1_deserialize(r.take(gs), compressed != 0, true), p->opening_proofs[i]);
+    const uint64_t nf = r.u64();
+    if (nf != no) throw Error(TNS_ERR_INVALID_PARAMETERS, "final evaluations do not match the openings");
+    for (uint64_t i = 0; i < nf; i++) {
+      const Fr v = fr_deserialize(r.take(32));
+      std::memcpy(p->final_evaluations[i], &v, 32);
+    }
+    if (r.n != len) throw Error(TNS_ERR_INVALID_PARAMETERS, "trailing bytes after the proof");
+    return TNS_OK;
+  });
+}
+
 // ---------------------------------------------------------------- communicators
 int tns_comm_unique_id(uint8_t uid[128]) {
   return guarded([&]() {

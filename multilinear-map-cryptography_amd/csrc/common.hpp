@@ -380,6 +380,12 @@ bool protocol_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine
                           const char *label1, const G1Affine C[2], const Fr *rounds, unsigned nv,
                           const Fr &final_eval, unsigned n_openings, const G1Affine pi[2], const Fr vals[2]);
 
+// serialize.cpp: ark-serialize 0.4 canonical encodings (host)
+void g1_serialize(const G1Affine &P, bool compressed, uint8_t *out);
+G1Affine g1_deserialize(const uint8_t *in, bool compressed, bool validate);
+void fr_serialize(const Fr &x, uint8_t out[32]);
+Fr fr_deserialize(const uint8_t in[32]);
+
 // host-side helpers (transcript.cpp)
 struct HostTranscript {
   std::vector<uint8_t> state;

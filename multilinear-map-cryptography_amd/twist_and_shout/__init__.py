@@ -355,6 +355,13 @@ class KZGCommitmentValue:
     commitment: G1Affine
     _proj: np.ndarray = field(repr=False, default=None, compare=False)
 
+    def serialize(self, compressed: bool = True) -> bytes:
+        return g1_serialize(self.commitment, compressed)
+
+    @staticmethod
+    def deserialize(data: bytes, compressed: bool = True) -> "KZGCommitmentValue":
+        return KZGCommitmentValue(g1_deserialize(data, compressed))
+
     def hash(self) -> int:
         out = np.zeros(4, dtype=np.uint64)
         proj = self._proj if self._proj is not None else _affine_to_proj(self.commitment)
@@ -366,6 +373,27 @@ class KZGCommitmentValue:
 class KZGProof:
     """src/commitments.rs:89-91"""
     proof: G1Affine
+
+    def serialize(self, compressed: bool = True) -> bytes:
+        return g1_serialize(self.proof, compressed)
+
+    @staticmethod
+    def deserialize(data: bytes, compressed: bool = True) -> "KZGProof":
+        return KZGProof(g1_deserialize(data, compressed))
+
+
+def g1_serialize(P: G1Affine, compressed: bool = True) -> bytes:
+    """ark-serialize 0.4 encoding of a G1 point (src/commitments.rs:94-154)."""
+    out = (C.c_uint8 * (32 if compressed else 64))()
+    _check(N.load().tns_g1_serialize(N.p64(_affine_to_proj(P)), 1 if compressed else 0, out))
+    return bytes(out)
+
+
+def g1_deserialize(data: bytes, compressed: bool = True) -> G1Affine:
+    buf = (C.c_uint8 * len(data)).from_buffer_copy(data)
+    proj = np.zeros(12, dtype=np.uint64)
+    _check(N.load().tns_g1_deserialize(buf, 1 if compressed else 0, N.p64(proj)))
+    return _g1_from_proj(proj)
 
 
 def _affine_to_proj(P: G1Affine) -> np.ndarray:
@@ -658,6 +686,18 @@ class TwistProof:
     sumcheck_challenges: List[int] = field(default_factory=list)
     final_mle_evals: List[int] = field(default_factory=list)
 
+    def serialize(self, compressed: bool = True) -> bytes:
+        """Wire format: fields in declaration order (src/twist.rs:76-89), Vec = u64 length + items."""
+        return _serialize_raw(_pack_proof(
+            [self.address_commitment.commitment, self.value_commitment.commitment],
+            self.consistency_proof.round_polynomials, self.consistency_proof.final_evaluation,
+            [p.proof for p in self.opening_proofs], self.final_evaluations), compressed)
+
+    @staticmethod
+    def deserialize(data: bytes, compressed: bool = True) -> "TwistProof":
+        u = _unpack_proof(_deserialize_raw(data, compressed), 3)
+        return TwistProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"])
+
 
 def _pack_proof(commitments, rounds, final_eval, openings, finals) -> N.TnsProof:
     """Proof fields (affine points / ints) -> the C proof struct (for the verifiers)."""
@@ -675,6 +715,21 @@ def _pack_proof(commitments, rounds, final_eval, openings, finals) -> N.TnsProof
         pr.opening_proofs[i] = (C.c_uint64 * 12)(*_affine_to_proj(o))
     for i, v in enumerate(finals):
         pr.final_evaluations[i] = (C.c_uint64 * 4)(*to_mont([v])[0])
+    return pr
+
+
+def _serialize_raw(pr: N.TnsProof, compressed: bool) -> bytes:
+    n = C.c_size_t()
+    _check(N.load().tns_proof_serialize(C.byref(pr), 1 if compressed else 0, None, 0, C.byref(n)))
+    buf = (C.c_uint8 * n.value)()
+    _check(N.load().tns_proof_serialize(C.byref(pr), 1 if compressed else 0, buf, n.value, C.byref(n)))
+    return bytes(buf)
+
+
+def _deserialize_raw(data: bytes, compressed: bool) -> N.TnsProof:
+    pr = N.TnsProof()
+    buf = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
+    _check(N.load().tns_proof_deserialize(buf, len(data), 1 if compressed else 0, C.byref(pr)))
     return pr
 
 
@@ -778,6 +833,18 @@ class ShoutProof:
     final_evaluations: List[int]
     opening_point: Optional[int] = None
     sumcheck_challenges: List[int] = field(default_factory=list)
+
+    def serialize(self, compressed: bool = True) -> bytes:
+        """Wire format: fields in declaration order (src/shout.rs:64-79)."""
+        return _serialize_raw(_pack_proof(
+            [self.table_commitment.commitment, self.index_commitment.commitment],
+            self.lookup_proof.round_polynomials, self.lookup_proof.final_evaluation,
+            [p.proof for p in self.opening_proofs], self.final_evaluations), compressed)
+
+    @staticmethod
+    def deserialize(data: bytes, compressed: bool = True) -> "ShoutProof":
+        u = _unpack_proof(_deserialize_raw(data, compressed), 1)
+        return ShoutProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"])
 
 
 class Shout:

@@ -131,6 +131,10 @@ SIGNATURES = [
     ("tns_shout_verify", C.c_int, [C.POINTER(TnsVk), C.POINTER(TnsProof), C.POINTER(C.c_int)]),
     ("tns_pairing", C.c_int, [U64P, U64P, U64P]),
     ("tns_g2_mul", C.c_int, [U64P, U64P, U64P]),
+    ("tns_g1_serialize", C.c_int, [U64P, C.c_int, U8P]),
+    ("tns_g1_deserialize", C.c_int, [U8P, C.c_int, U64P]),
+    ("tns_proof_serialize", C.c_int, [C.POINTER(TnsProof), C.c_int, U8P, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("tns_proof_deserialize", C.c_int, [U8P, C.c_size_t, C.c_int, C.POINTER(TnsProof)]),
     ("tns_bench_trace_slice", C.c_int, [C.c_size_t, C.c_uint64, C.c_uint64, C.c_size_t, U64P, U64P, U8P]),
     ("tns_comm_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("tns_comm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),

@@ -943,3 +943,36 @@ def protocol_verify(vk, seed, labels, C, rounds, final_eval, openings, values):
             if not kzg_verify(vk, C[k], z[0], values[k], openings[k]):
                 return False
     return True
+
+
+# ----------------------------------------------------------------------------
+# Canonical serialisation (ark-serialize 0.4.2 / ark-ec 0.4.2 short-Weierstrass Affine,
+# used by src/commitments.rs:94-154): x (and y) little-endian, SWFlags in the top bits of
+# the last byte: YIsNegative = 0x80 (y > -y), PointAtInfinity = 0x40.
+# ----------------------------------------------------------------------------
+def g1_serialize(P, compressed=True):
+    n = 32 if compressed else 64
+    if P is None:
+        out = bytearray(n)
+        out[-1] |= 0x40
+        return bytes(out)
+    x, y = P
+    out = bytearray(x.to_bytes(32, "little") + (b"" if compressed else y.to_bytes(32, "little")))
+    if y > (P_MOD - y) % P_MOD:
+        out[-1] |= 0x80
+    return bytes(out)
+
+
+def fr_serialize(x):
+    return (x % R_MOD).to_bytes(32, "little")
+
+
+def proof_serialize(commitments, rounds, final_eval, openings, finals, compressed=True):
+    """Twist/ShoutProof fields in declaration order; Vec<T> = u64 LE length + elements."""
+    u64 = lambda v: int(v).to_bytes(8, "little")  # noqa: E731
+    out = b"".join(g1_serialize(C, compressed) for C in commitments)
+    out += u64(len(rounds)) + b"".join(u64(len(r)) + b"".join(fr_serialize(c) for c in r) for r in rounds)
+    out += fr_serialize(final_eval)
+    out += u64(len(openings)) + b"".join(g1_serialize(P, compressed) for P in openings)
+    out += u64(len(finals)) + b"".join(fr_serialize(v) for v in finals)
+    return out
