@@ -138,12 +138,18 @@ int tns_kzg_open(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, size_
                  const uint64_t z[4], uint64_t value[4], uint64_t proof_proj[12]);
 /* commit(vector_to_polynomial(evals)) and open(vector_to_polynomial(evals), z) in one
  * step (src/polynomials.rs:248-262 then src/commitments.rs:162-199), as Twist/Shout::prove
- * do: through the SRS's Lagrange basis when it has tau, else by interpolation.  n must
- * be a power of two (the provers pad to one, src/twist.rs:141). */
+ * do: through the SRS's Lagrange basis when it has tau, else by interpolation (which needs
+ * n to be a power of two, as the provers pad to, src/twist.rs:141). */
 int tns_kzg_commit_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n,
                          uint64_t out_proj[12]);
 int tns_kzg_open_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, size_t n,
                        const uint64_t z[4], uint64_t value[4], uint64_t proof_proj[12]);
+/* KZGVectorCommitment::open (src/commitments.rs:440-471): the opening of the vector's
+ * interpolant at the node `index` (value = vec[index]); commit = tns_kzg_commit_evals (any n
+ * when the SRS carries tau); verify = tns_kzg_verify at z = index.  index >= n ->
+ * TNS_ERR_COMMITMENT ("Index out of bounds"). */
+int tns_vc_open(tns_ctx *ctx, const tns_srs *srs, const uint64_t *vec, size_t n, size_t index, uint64_t value[4],
+                uint64_t proof_proj[12]);
 /* KZGCommitmentValue::hash (src/commitments.rs:73-84).  Host only. */
 int tns_commitment_hash(const uint64_t proj[12], uint64_t out[4]);
 /* Raw MSM: sum_i scalars[i] * points[i] over the first n SRS points. */

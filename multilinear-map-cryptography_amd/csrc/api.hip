@@ -130,6 +130,8 @@ static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p, Comm &m) {
     return xyzz_to_affine(allgather_sum_g1(c, m, part));
   }
   if (m.size > 1) throw Error(TNS_ERR_INVALID_PARAMETERS, "sharded proving needs an SRS with tau (Lagrange basis)");
+  if (p.N & (p.N - 1))
+    throw Error(TNS_ERR_POLYNOMIAL, "interpolation of a non-power-of-two vector needs an SRS with tau (Lagrange basis)");
   interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
   p.have_coeffs = true;
   return commit_dev(c, srs, p.coeffs, p.N);
@@ -137,6 +139,14 @@ static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p, Comm &m) {
 
 static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *value, G1Affine *proof,
                        DevBuf &sbuf, Comm &m) {
+  if (p.basis && m.size == 1 && fr_is_node(z, p.N)) {  // z = j0 is a node: value y_j0, derivative term
+    const size_t j0 = (size_t)from_mont(z).v[0];
+    Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.N);
+    TNS_HIP(hipMemcpyAsync(value, p.y + j0, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+    lagrange_node_quotient_dev(c, p.y, p.N, j0, q);  // synchronises
+    *proof = xyzz_to_affine(msm_dev(c, p.basis->points.as<G1Affine>(), q, p.N, p.basis->fb));
+    return;
+  }
   if (p.basis && !fr_is_node(z, p.N)) {
     Fr *q = (Fr *)sbuf.ensure(sizeof(Fr) * p.cnt);
     Fr part[2];
@@ -160,7 +170,9 @@ static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *val
   }
   if (m.size > 1)  // z on a node: probability ~2^-230; the coefficient route is unsharded
     throw Error(TNS_ERR_PROOF_GENERATION, "opening challenge is an interpolation node (sharded prover)");
-  if (!p.have_coeffs) {  // z is a node (or no basis): coefficient form
+  if (!p.have_coeffs) {  // no basis: coefficient form
+    if (p.N & (p.N - 1))
+      throw Error(TNS_ERR_POLYNOMIAL, "interpolation of a non-power-of-two vector needs an SRS with tau (Lagrange basis)");
     interpolate_consecutive_dev(c, p.y, p.N, p.coeffs);
     p.have_coeffs = true;
   }
@@ -448,7 +460,7 @@ int tns_kzg_commit(tns_ctx *ctx, const tns_srs *srs, const uint64_t *coeffs, siz
 }
 
 static void upload_evals(tns_ctx *ctx, const uint64_t *evals, size_t n, DevBuf &d, DevBuf &cf, EvalPoly &p) {
-  if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_POLYNOMIAL, "evaluation vector length must be a power of two");
+  if (n == 0) throw Error(TNS_ERR_POLYNOMIAL, "empty evaluation vector");
   Fr *dy = (Fr *)d.ensure(sizeof(Fr) * n);
   TNS_HIP(hipMemcpyAsync(dy, evals, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
   p.y = dy;
@@ -482,6 +494,28 @@ int tns_kzg_open_evals(tns_ctx *ctx, const tns_srs *srs, const uint64_t *evals, 
     std::memcpy(&zz, z, 32);
     G1Affine pi;
     open_evals(&ctx->c, srs->s, p, zz, &v, &pi, s, comm_self());
+    std::memcpy(value, &v, 32);
+    store_proj(pi, proof);
+    return TNS_OK;
+  });
+}
+
+// KZGVectorCommitment (src/commitments.rs:408-483): commit = commit(interpolant of v on
+// 0..n-1), any n; open at index i = KZG open at the node i (value v_i).
+int tns_vc_open(tns_ctx *ctx, const tns_srs *srs, const uint64_t *vec, size_t n, size_t index, uint64_t value[4],
+                uint64_t proof[12]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    if (index >= n) throw Error(TNS_ERR_COMMITMENT, "Index out of bounds");
+    DevBuf d, cf, s;
+    EvalPoly p;
+    upload_evals(ctx, vec, n, d, cf, p);
+    if (n > srs->s.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+    p.basis = lagrange_basis_dev(&ctx->c, srs->s, n, 0, n);
+    const Fr z = from_u64<FrCfg>((uint64_t)index);
+    Fr v;
+    G1Affine pi;
+    open_evals(&ctx->c, srs->s, p, z, &v, &pi, s, comm_self());
     std::memcpy(value, &v, 32);
     store_proj(pi, proof);
     return TNS_OK;

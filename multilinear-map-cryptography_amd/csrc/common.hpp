@@ -133,8 +133,8 @@ struct Srs {
   // also yields the Lagrange basis of the nodes {0..N-1}: G * L_j(tau) (lagrange.hip).
   bool has_tau = false;
   Fr tau;
-  // (log N, first node, node count) -> basis slice (cache)
-  mutable std::map<std::tuple<unsigned, size_t, size_t>, LagrangeBasis *> lagrange;
+  // (N, first node, node count) -> basis slice (cache)
+  mutable std::map<std::tuple<size_t, size_t, size_t>, LagrangeBasis *> lagrange;
   size_t first = 0, held = 0;  // points[0..held) are g1_powers[first .. first + held) (sharded SRS)
   mutable FixedBase *fb = nullptr;                        // window table of `points` (lazy)
   Srs() = default;
@@ -243,7 +243,7 @@ struct Ctx {
   unsigned twiddle_log = 0;
   std::vector<InterpPlan *> plans;  // indexed by log_n
   std::map<uint32_t, DevBuf *> pass_tw;  // four-step pass twiddles keyed by (lo << 8 | r)
-  std::map<std::tuple<unsigned, size_t, size_t>, DevBuf *> bary_w;  // (log N, first, count) -> weights
+  std::map<std::tuple<size_t, size_t, size_t>, DevBuf *> bary_w;  // (N, first, count) -> weights
   bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
   bool msm_tables = true;                // shared-bucket MSM on fixed bases with window tables
   KernelProfiler prof;
@@ -339,6 +339,8 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
                                Fr *ell_part, Fr *sum_part);
 // q_i = (v - y_i) * inv_i in place: the quotient's values on the slice
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
+// quotient values for an opening AT the node j0 (value y_j0), unsharded
+void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q);
 bool fr_is_node(const Fr &x, size_t N);
 
 // comm.cpp: the exchange steps of a sharded proof

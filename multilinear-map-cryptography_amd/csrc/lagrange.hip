@@ -23,6 +23,7 @@
 // product of the chain products.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <tuple>
 #include <vector>
 
@@ -32,16 +33,17 @@ namespace tns {
 
 constexpr unsigned NODE_THREADS = 512 * 256;  // batch-inversion chains (one Fermat inverse each)
 
-// chain t: elements i = t + k*T.  pre[i] = prod of earlier (x - i') of the chain; cp[t] = chain product
-__global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr Tm, Fr *__restrict__ pre,
-                                                    Fr *__restrict__ cp) {
+// chain t: elements i = t + k*T.  pre[i] = prod of earlier (x - i') of the chain; cp[t] = chain
+// product.  Node `skip` (x itself, when opening at a node) contributes the factor 1.
+__global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr Tm, size_t skip,
+                                                    Fr *__restrict__ pre, Fr *__restrict__ cp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t >= T) return;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)t));  // x - i, stepping by -T
   Fr acc = Fr::one();
   for (size_t i = t; i < n; i += T) {
     pre[i] = acc;
-    acc = mul(acc, d);
+    if (i != skip) acc = mul(acc, d);
     d = sub(d, Tm);
   }
   cp[t] = acc;
@@ -62,14 +64,15 @@ __global__ void __launch_bounds__(1024) k_prod_reduce(const Fr *__restrict__ in,
 }
 
 // Backward sweep of chain t: inv_i = 1/(x - i) from pre[i] and the chain inverse.
-//   BASIS: out[i] = canonical(ell * w_i * inv_i)            (Lagrange scalars L_i(x))
-//   OPEN:  out[i] = inv_i, sp[t] = sum_chain w_i y_i inv_i  (barycentric partial sum)
+//   BASIS: out[i] = canonical(ell * w_i * inv_i)                  (Lagrange scalars L_i(x))
+//   OPEN:  out[i] = inv_i, sp[t] = sum_chain w_i (y_i - yoff) inv_i (barycentric partial sum)
+// The punctured node `skip` (opening at a node) gets inv 0 and no sum term.
 template <bool BASIS>
 // (pre and out may alias: each element's pre is read before its output is written)
-__global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
-                                                     const Fr *__restrict__ cp, const Fr *__restrict__ w,
-                                                     const Fr *__restrict__ y, const Fr *__restrict__ ell,
-                                                     Fr *out, Fr *__restrict__ sp) {
+__global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, Fr Tm, size_t skip, Fr yoff,
+                                                     const Fr *pre, const Fr *__restrict__ cp,
+                                                     const Fr *__restrict__ w, const Fr *__restrict__ y,
+                                                     const Fr *__restrict__ ell, Fr *out, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t >= T) return;
   if (t >= n) {
@@ -83,13 +86,14 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
   Fr s = Fr::zero();
   const Fr L = BASIS ? ell[0] : Fr::one();
   for (;;) {
-    const Fr inv_i = mul(iv, pre[i]);
-    iv = mul(iv, d);
+    const bool hole = i == skip;
+    const Fr inv_i = hole ? Fr::zero() : mul(iv, pre[i]);
+    if (!hole) iv = mul(iv, d);
     if (BASIS) {
       out[i] = from_mont(mul(mul(L, w[i]), inv_i));
     } else {
       out[i] = inv_i;
-      s = add(s, mul(mul(w[i], y[i]), inv_i));
+      s = add(s, mul(mul(w[i], sub(y[i], yoff)), inv_i));
     }
     if (i < T) break;
     i -= T;
@@ -143,7 +147,7 @@ __global__ void __launch_bounds__(1024) k_sum_reduce(const Fr *__restrict__ in, 
 
 // barycentric weights of the nodes [first, first + cnt) of {0..N-1} (cached per slice)
 static const Fr *bary_weights(Ctx *c, size_t N, size_t first, size_t cnt) {
-  const auto key = std::make_tuple(ilog2_exact(N), first, cnt);
+  const auto key = std::make_tuple(N, first, cnt);
   auto it = c->bary_w.find(key);
   if (it != c->bary_w.end()) return it->second->as<Fr>();
   DevBuf fact, ifact;
@@ -175,7 +179,7 @@ struct NodeSweep {
 };
 
 // chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
-static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre) {
+static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_t skip = SIZE_MAX) {
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
@@ -183,7 +187,7 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre) {
   s.cp = ws;
   s.sp = ws + s.T;
   s.dev = ws + 2 * s.T;
-  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, pre, s.cp);
+  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp);
   TNS_LAUNCH_CHECK();
   k_prod_reduce<<<1, 1024, 0, c->stream>>>(s.cp, s.T, s.dev);
   TNS_LAUNCH_CHECK();
@@ -193,10 +197,10 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre) {
 static Fr fr_shift(const Fr &x, size_t first) { return sub(x, from_u64<FrCfg>((uint64_t)first)); }
 
 const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t first, size_t cnt) {
-  if (!c->lagrange_commit || !srs.has_tau || N == 0 || (N & (N - 1))) return nullptr;
+  if (!c->lagrange_commit || !srs.has_tau || N == 0) return nullptr;
   if (first + cnt > N || cnt == 0) throw Error(TNS_ERR_INVALID_PARAMETERS, "node slice outside 0..N-1");
   if (fr_is_node(srs.tau, N)) return nullptr;
-  const auto key = std::make_tuple(ilog2_exact(N), first, cnt);
+  const auto key = std::make_tuple(N, first, cnt);
   auto it = srs.lagrange.find(key);
   if (it != srs.lagrange.end()) return it->second;
   const Fr *w = bary_weights(c, N, first, cnt);
@@ -213,8 +217,8 @@ const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t
   Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * cnt);  // pre, then canonical L_j(tau) in place
   const Fr xs = fr_shift(srs.tau, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, sc);
-  k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, sc, s.cp, w, nullptr,
-                                                                           ecp + TG, sc, nullptr);
+  k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
+                                                                           sc, s.cp, w, nullptr, ecp + TG, sc, nullptr);
   TNS_LAUNCH_CHECK();
   LagrangeBasis *b = new LagrangeBasis();
   try {
@@ -235,8 +239,8 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
   const Fr *w = bary_weights(c, N, first, cnt);
   const Fr xs = fr_shift(z, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
-  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.cp, w, y,
-                                                                            nullptr, inv, s.sp);
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
+                                                                            inv, s.cp, w, y, nullptr, inv, s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
   TNS_LAUNCH_CHECK();
@@ -245,6 +249,33 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
   TNS_HIP(hipStreamSynchronize(c->stream));
   *ell_part = h[0];
   *sum_part = h[1];
+}
+
+// Opening at the node j0 (KZGVectorCommitment::open, src/commitments.rs:440-471): the quotient
+// (P(x) - y_j0) / (x - j0) has values q_j = (y_j0 - y_j) / (j0 - j) at j != j0 and
+// q_j0 = P'(j0) = (1 / w_j0) sum_{j != j0} w_j (y_j - y_j0) / (j0 - j) (barycentric derivative).
+void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q) {
+  TNS_PROF(c, "open_scan", 32.0 * 6 * N);
+  const Fr *w = bary_weights(c, N, 0, N);
+  Fr v;
+  TNS_HIP(hipMemcpyAsync(&v, y + j0, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  const Fr xs = from_u64<FrCfg>((uint64_t)j0);
+  NodeSweep s = node_sweep_begin(c, xs, N, q, j0);
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, N, s.T, s.Tm, j0, v, q, s.cp, w, y,
+                                                                            nullptr, q, s.sp);
+  TNS_LAUNCH_CHECK();
+  k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
+  TNS_LAUNCH_CHECK();
+  k_node_quotient<<<grid_for(N, 256), 256, 0, c->stream>>>(y, v, N, q);  // q_j0 = (v - y_j0) * 0 = 0 for now
+  TNS_LAUNCH_CHECK();
+  Fr h[2], wj;
+  TNS_HIP(hipMemcpyAsync(h, s.dev, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipMemcpyAsync(&wj, w + j0, sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  const Fr qj0 = mul(h[1], inv(wj));
+  TNS_HIP(hipMemcpyAsync(q + j0, &qj0, sizeof(Fr), hipMemcpyHostToDevice, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
 }
 
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q) {

@@ -481,6 +481,29 @@ class KZGCommitment:
         return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
 
 
+class KZGVectorCommitment:
+    """``impl VectorCommitmentScheme for KZGVectorCommitment`` (src/commitments.rs:408-483):
+    KZG over the interpolant of the vector on the nodes 0..n-1."""
+
+    @staticmethod
+    def commit(params: CommitmentParams, vector) -> KZGCommitmentValue:
+        return KZGCommitment.commit_evaluations(params, vector)
+
+    @staticmethod
+    def open(params: CommitmentParams, vector, index: int) -> Tuple[int, KZGProof]:
+        y = _as_mont(vector)
+        v = np.zeros(4, dtype=np.uint64)
+        pi = np.zeros(12, dtype=np.uint64)
+        _check(N.load().tns_vc_open(params.srs.ctx.handle, params.srs.handle, N.p64(_nonempty(y)), len(y), index,
+                                    N.p64(v), N.p64(pi)))
+        return from_mont(v)[0], KZGProof(_g1_from_proj(pi))
+
+    @staticmethod
+    def verify(vk: "CommitmentVerificationKey", commitment: KZGCommitmentValue, index: int, value: int,
+               proof: KZGProof) -> bool:
+        return KZGCommitment.verify(vk, commitment, index, value, proof)
+
+
 def msm(params: CommitmentParams, scalars) -> G1Affine:
     """Raw G1 MSM over the first len(scalars) SRS points (the commit kernel)."""
     c = _as_mont(scalars)
@@ -1155,5 +1178,6 @@ __all__ = [
     "KZGCommitmentValue", "KZGProof", "msm", "poly_utils", "MultilinearExtension", "SumCheck", "SumCheckProof",
     "MemoryOp", "MemoryTrace", "Twist", "TwistProof", "LookupOp", "LookupTable", "Shout", "ShoutProof",
     "bench_trace", "to_mont", "from_mont", "fr_from_u64_array", "device_count", "Comm", "setup_params_shard",
-    "shard_slice", "bench_trace_slice",
+    "shard_slice", "bench_trace_slice", "KZGVectorCommitment", "CommitmentVerificationKey", "pairing",
+    "g1_serialize", "g1_deserialize",
 ]

@@ -87,6 +87,7 @@ SIGNATURES = [
     ("tns_kzg_open", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
     ("tns_kzg_commit_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_kzg_open_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
+    ("tns_vc_open", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, C.c_size_t, U64P, U64P]),
     ("tns_commitment_hash", C.c_int, [U64P, U64P]),
     ("tns_msm", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_interpolate_consecutive", C.c_int, [C.c_void_p, U64P, C.c_size_t, U64P]),

@@ -184,7 +184,11 @@ def test_prepare_lagrange_errors():
     pp.commitment_params.srs.prepare_lagrange(16)
 
 
-def test_evaluations_length_must_be_power_of_two():
+def test_non_power_of_two_needs_tau_basis():
     pp, _ = params(3)
+    ys = [1, 2, 3]
+    got = ts.KZGCommitment.commit_evaluations(pp.commitment_params, ys).commitment
+    assert got == po.affine_mul(po.G1_GEN, po.barycentric_eval(ys, pp.commitment_params.tau))
+    cp = ts.CommitmentParams.from_g1_powers(pp.commitment_params.g1_powers)  # no tau: interpolation only
     with pytest.raises(ts.PolynomialError):
-        ts.KZGCommitment.commit_evaluations(pp.commitment_params, [1, 2, 3])
+        ts.KZGCommitment.commit_evaluations(cp, ys)
