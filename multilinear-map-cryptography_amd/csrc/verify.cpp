@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "hostfield.hpp"
 
 namespace tns {
 
@@ -18,16 +19,49 @@ static void canon64(const Fr &x, uint64_t out[4]) {
   for (int i = 0; i < 4; i++) out[i] = (uint64_t)c.v[2 * i] | ((uint64_t)c.v[2 * i + 1] << 32);
 }
 
-// k * P on the host (double-and-add over XYZZ), k a Montgomery-form Fr
-G1Xyzz g1_mul_host(const G1Xyzz &P, const Fr &k) {
+// k * P on the host: double-and-add over XYZZ in the 4 x u64 host field (hostfield.hpp),
+// k a Montgomery-form Fr.  dbl-2008-s-1 / madd-2008-s (a = 0).
+namespace {
+struct HX {
+  HFq x, y, zz, zzz;
+};
+HX hx_dbl(const HX &p) {
+  if (p.zz.is_zero()) return p;
+  const HFq U = p.y + p.y, V = U * U, W = U * V, S = p.x * V;
+  const HFq X2 = p.x * p.x, M = X2 + X2 + X2;
+  const HFq X3 = M * M - (S + S);
+  return HX{X3, M * (S - X3) - W * p.y, V * p.zz, W * p.zzz};
+}
+HX hx_madd(const HX &p, const HFq &x2, const HFq &y2) {
+  if (p.zz.is_zero()) return HX{x2, y2, HFq::one(), HFq::one()};
+  const HFq P = x2 * p.zz - p.x, R = y2 * p.zzz - p.y;
+  if (P.is_zero()) {
+    if (R.is_zero()) return hx_dbl(HX{x2, y2, HFq::one(), HFq::one()});
+    return HX{HFq::one(), HFq::one(), HFq::zero(), HFq::zero()};
+  }
+  const HFq PP = P * P, PPP = P * PP, Q = p.x * PP;
+  const HFq X3 = R * R - PPP - (Q + Q);
+  return HX{X3, R * (Q - X3) - p.y * PPP, p.zz * PP, p.zzz * PPP};
+}
+}  // namespace
+
+G1Xyzz g1_mul_host(const G1Affine &P, const Fr &k) {
+  if (P.is_inf()) return G1Xyzz::inf();
   uint64_t e[4];
   canon64(k, e);
-  G1Xyzz r = G1Xyzz::inf();
+  const HFq px = HFq::of(P.x), py = HFq::of(P.y);
+  HX r{HFq::one(), HFq::one(), HFq::zero(), HFq::zero()};
   for (int i = 255; i >= 0; i--) {
-    r = xyzz_dbl(r);
-    if ((e[i / 64] >> (i % 64)) & 1) r = xyzz_add(r, P);
+    r = hx_dbl(r);
+    if ((e[i / 64] >> (i % 64)) & 1) r = hx_madd(r, px, py);
   }
-  return r;
+  if (r.zz.is_zero()) return G1Xyzz::inf();
+  G1Xyzz out;
+  out.x = r.x.fp();
+  out.y = r.y.fp();
+  out.zz = r.zz.fp();
+  out.zzz = r.zzz.fp();
+  return out;
 }
 
 G1Affine g1_generator_host() {
@@ -48,7 +82,7 @@ void verifier_key(const Fr &tau, G1Affine *g1, G2Affine *g2, G2Affine *g2_tau) {
 // e(C - v G1, G2) == e(pi, tau G2 - z G2)   (src/commitments.rs:201-228)
 bool kzg_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine &g2_tau, const G1Affine &C,
                      const Fr &z, const Fr &v, const G1Affine &pi) {
-  const G1Xyzz left = xyzz_add(xyzz_from_affine(C), g1_mul_host(xyzz_from_affine(g1_neg(g1)), v));
+  const G1Xyzz left = xyzz_add(xyzz_from_affine(C), g1_mul_host(g1_neg(g1), v));
   uint64_t zc[4];
   canon64(z, zc);
   const G2Affine right = g2_add(g2_tau, g2_neg(g2_mul(g2, zc)));
@@ -69,16 +103,16 @@ bool kzg_batch_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affin
   bg2.x0 = bg2.x1 = bg2.y0 = bg2.y1 = Fq::zero();
   bg2.inf = true;
   for (size_t i = 0; i < n; i++) {
-    bc = xyzz_add(bc, g1_mul_host(xyzz_from_affine(C[i]), gam[i]));
+    bc = xyzz_add(bc, g1_mul_host(C[i], gam[i]));
     bv = add(bv, mul(v[i], gam[i]));
-    bp = xyzz_add(bp, g1_mul_host(xyzz_from_affine(pi[i]), gam[i]));
+    bp = xyzz_add(bp, g1_mul_host(pi[i], gam[i]));
     uint64_t zc[4], gc[4];
     canon64(z[i], zc);
     canon64(gam[i], gc);
     const G2Affine t = g2_add(g2_tau, g2_neg(g2_mul(g2, zc)));
     bg2 = g2_add(bg2, g2_mul(t, gc));
   }
-  const G1Xyzz left = xyzz_add(bc, g1_mul_host(xyzz_from_affine(g1_neg(g1)), bv));
+  const G1Xyzz left = xyzz_add(bc, g1_mul_host(g1_neg(g1), bv));
   return pairing_eq(xyzz_to_affine(left), g2, xyzz_to_affine(bp), bg2);
 }
 
