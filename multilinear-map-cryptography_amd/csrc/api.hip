@@ -223,8 +223,17 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
   }
   Fr *q0 = (Fr *)sbuf0.ensure(sizeof(Fr) * p0.cnt), *q1 = (Fr *)sbuf1.ensure(sizeof(Fr) * p1.cnt);
   Fr part[4];
-  lagrange_open_partial_dev(c, p0.y, p0.N, p0.first, p0.cnt, z, q0, &part[0], &part[1]);
-  lagrange_open_partial_dev(c, p1.y, p1.N, p1.first, p1.cnt, z, q1, &part[2], &part[3]);
+  const bool same_nodes = p0.N == p1.N && p0.first == p1.first && p0.cnt == p1.cnt;
+  if (same_nodes) {  // Twist: one batch inversion for both vectors (inverses land in q1)
+    Fr p3[3];
+    lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3);
+    part[0] = part[2] = p3[0];
+    part[1] = p3[1];
+    part[3] = p3[2];
+  } else {
+    lagrange_open_partial_dev(c, p0.y, p0.N, p0.first, p0.cnt, z, q0, &part[0], &part[1]);
+    lagrange_open_partial_dev(c, p1.y, p1.N, p1.first, p1.cnt, z, q1, &part[2], &part[3]);
+  }
   Fr ell[2] = {Fr::one(), Fr::one()}, S[2] = {Fr::zero(), Fr::zero()};
   const std::vector<Fr> all = allgather_fr(c, m, part, 4);
   for (int r = 0; r < m.size; r++)
@@ -233,8 +242,12 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
       S[k] = add(S[k], all[4 * (size_t)r + 2 * k + 1]);
     }
   for (int k = 0; k < 2; k++) value[k] = mul(ell[k], S[k]);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
-  lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
-  lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
+  if (same_nodes) {
+    lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1);
+  } else {
+    lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
+    lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
+  }
   G1Xyzz pp[2];
   msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb},
                MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb}, pp);
@@ -299,7 +312,16 @@ int tns_ctx_create(int device, tns_ctx **out) {
     x->c.device = device;
     TNS_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
     x->c.lanes[0].stream = x->c.stream;
-    TNS_HIP(hipStreamCreateWithFlags(&x->c.lanes[1].stream, hipStreamNonBlocking));
+    int prio_lo = 0, prio_hi = 0;
+    TNS_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    const char *st = getenv("TNS_MSM_STAGGER");
+    x->c.msm_stagger = st && st[0] == '1';
+    x->c.num_cu = prop.multiProcessorCount;
+    if (const char *aw = getenv("TNS_ACC_WAVES")) x->c.acc_waves = atoi(aw);
+    const char *cs = getenv("TNS_MSM_SORT");
+    x->c.msm_cub_sort = cs && std::string(cs) == "cub";
+    TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking,
+                                        x->c.msm_stagger ? prio_hi : prio_lo));
     *out = x;
     return TNS_OK;
   });

@@ -36,6 +36,8 @@ struct FrCfg {
   static constexpr u32 R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
                                 0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
   static constexpr u32 INV = 0xefffffffu;
+  static constexpr u32 M2[8] = {0xe0000002u, 0x87c3eb27u, 0xf372e122u, 0x5067d090u,
+                                0x0302b0bau, 0x70a08b6du, 0xc2634053u, 0x60c89ce5u};  // 2M
 };
 struct FqCfg {
   static constexpr u32 M[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
@@ -45,6 +47,8 @@ struct FqCfg {
   static constexpr u32 R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
                                 0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
   static constexpr u32 INV = 0xe4866389u;
+  static constexpr u32 M2[8] = {0xb0f9fa8eu, 0x7841182du, 0xd0e3951au, 0x2f02d522u,
+                                0x0302b0bbu, 0x70a08b6du, 0xc2634053u, 0x60c89ce5u};  // 2M
 };
 
 template <class C>
@@ -81,10 +85,18 @@ struct alignas(16) Fp {
 typedef Fp<FrCfg> Fr;
 typedef Fp<FqCfg> Fq;
 
+#if defined(__HIPCC__)
+#include "field_asm.inc"
+#endif
+
 // ---------------------------------------------------------------- raw 256-bit helpers
 // r = a - M if a >= M (a < 2M assumed)
 template <class C>
 TNS_HD void reduce_once(Fp<C> &a) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_NO_FIELD_ASM)
+  reduce_once_dev(a);
+  return;
+#endif
   u32 t[8];
   u64 br = 0;
 #pragma unroll
@@ -101,6 +113,9 @@ TNS_HD void reduce_once(Fp<C> &a) {
 
 template <class C>
 TNS_HD Fp<C> add(const Fp<C> &a, const Fp<C> &b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_NO_FIELD_ASM)
+  return add_dev(a, b);
+#endif
   Fp<C> r;
   u64 c = 0;
 #pragma unroll
@@ -115,6 +130,9 @@ TNS_HD Fp<C> add(const Fp<C> &a, const Fp<C> &b) {
 
 template <class C>
 TNS_HD Fp<C> sub(const Fp<C> &a, const Fp<C> &b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_NO_FIELD_ASM)
+  return sub_dev(a, b);
+#endif
   Fp<C> r;
   u64 br = 0;
 #pragma unroll
@@ -155,7 +173,11 @@ TNS_HD Fp<C> dbl(const Fp<C> &a) {
 }
 
 #if defined(__HIPCC__)
+#ifdef TNS_MONT_MUL_INC  // benchmark builds (tools/maddbench.hip) swap the product variant
+#include TNS_MONT_MUL_INC
+#else
 #include "mont_mul.inc"
+#endif
 #endif
 
 // Host (and reference): CIOS Montgomery product, no-carry variant (top modulus limb < 2^31 - 1).
@@ -365,6 +387,60 @@ TNS_HD G1Xyzz xyzz_madd(const G1Xyzz &p, const G1Affine &q) {
   r.zzz = mul(p.zzz, PPP);
   return r;
 }
+
+#if defined(__HIPCC__)
+// ---- lazy-reduction mixed addition for the MSM accumulation (device only).  Coordinates of
+// the running sum live in [0, 2M): products skip their final conditional subtraction
+// (inputs < 2M give results < 2M since 4M < 2^256), sums and differences reduce against 2M,
+// and "is zero mod M" is {0, M}.  The affine input is canonical; xyzz_canon brings a sum
+// back to [0, M) before anything else reads it.
+__device__ __forceinline__ bool fq_zero_lazy(const Fq &a) {
+  u32 z = 0, m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    z |= a.v[i];
+    m |= a.v[i] ^ FqCfg::M[i];
+  }
+  return z == 0 || m == 0;
+}
+
+__device__ __forceinline__ G1Xyzz xyzz_madd_lazy(const G1Xyzz &p, const G1Affine &q) {
+  if (q.is_inf()) return p;
+  if (p.is_inf()) {
+    G1Xyzz r;
+    r.x = q.x;
+    r.y = q.y;
+    r.zz = Fq::one();
+    r.zzz = Fq::one();
+    return r;
+  }
+  const Fq U2 = mul_lazy_dev(q.x, p.zz);
+  const Fq S2 = mul_lazy_dev(q.y, p.zzz);
+  const Fq P = sub2_dev(U2, p.x);
+  const Fq R = sub2_dev(S2, p.y);
+  if (fq_zero_lazy(P)) {
+    if (fq_zero_lazy(R)) return xyzz_mdbl(q);
+    return G1Xyzz::inf();
+  }
+  const Fq PP = mul_lazy_dev(P, P);
+  const Fq PPP = mul_lazy_dev(P, PP);
+  const Fq Q = mul_lazy_dev(p.x, PP);
+  G1Xyzz r;
+  r.x = sub2_dev(sub2_dev(mul_lazy_dev(R, R), PPP), add2_dev(Q, Q));
+  r.y = sub2_dev(mul_lazy_dev(R, sub2_dev(Q, r.x)), mul_lazy_dev(p.y, PPP));
+  r.zz = mul_lazy_dev(p.zz, PP);
+  r.zzz = mul_lazy_dev(p.zzz, PPP);
+  return r;
+}
+
+__device__ __forceinline__ G1Xyzz xyzz_canon(G1Xyzz p) {
+  reduce_once_dev(p.x);
+  reduce_once_dev(p.y);
+  reduce_once_dev(p.zz);
+  reduce_once_dev(p.zzz);
+  return p;
+}
+#endif
 
 // add-2008-s: XYZZ + XYZZ
 TNS_HD G1Xyzz xyzz_add(const G1Xyzz &p, const G1Xyzz &q) {

@@ -1,0 +1,377 @@
+// bucket_sort.hip -- the MSM's (bucket, point) ordering: signed-window digits fused into a
+// most-significant-digit-first counting sort.
+//
+// k_accumulate (msm.hip) needs the W*n (bucket, point|sign) entries of an MSM grouped by
+// bucket.  A general radix sort (rocPRIM onesweep) spends a digit kernel, a histogram pass
+// and one full read+write of keys and values per 8-bit digit on it.  Here:
+//  * pass 1 reads the SCALARS (32 B each, W entries per scalar), recomputes their digits in
+//    registers and scatters the entries straight into bins of the top key bits -- the
+//    digit array never exists, and zero digits never enter the sort;
+//  * passes 2.. split each bin by the next key bits.  MSD order needs no stability, so a
+//    pass is per-tile LDS histograms + one exclusive scan + a scatter; tiles never cross a
+//    bin, so a skewed bin (every scalar with the same digit) is just many tiles of one bin;
+//  * every scatter first orders its tile by bin in LDS, then writes each bin's run with
+//    consecutive lanes (coalesced stores instead of one scattered 4-B store per entry);
+//  * the last pass's bin boundaries are the bucket bounds.
+// Shared-bucket layout (fixed-base window tables): the key is (bucket, window), so inside a
+// bucket the entries come window by window.  The accumulation gathers its points from the
+// window's slab of the 12.9 GB table (T[w n + i]); window-major runs keep the slabs a wave
+// touches at once few (entries of all 12 slabs mixed cost k_accumulate ~30 %).  The order
+// inside one (bucket, window) run is unspecified (LDS atomics): bucket sums are group
+// elements, so the MSM result does not depend on it.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace tns {
+
+constexpr int BS_BLOCK = 256;  // 4 waves: fits the slots k_accumulate leaves free
+constexpr int BS_MAXBITS = 9;  // key bits per pass
+constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
+constexpr int BS_TILE = 8192;  // entries per tile (LDS staging: 64 KiB)
+constexpr int BS_IPT = BS_TILE / BS_BLOCK;
+constexpr int BS_SCALARS = 4;  // scalars a pass-1 thread loads ahead
+
+
+struct DigitArgs {
+  const Fr *scalars;
+  size_t n, spb;  // scalars, scalars per tile (spb * W <= BS_TILE)
+  int c, W, wb;   // window bits, windows, window-index bits appended to the key (shared)
+  bool shared;
+  uint32_t stride;
+};
+
+// signed c-bit digits of scalar i (msm.hip k_digits): f(key, value) for every non-zero digit;
+// shared: key = (|d| - 1) << wb | w, value = (w * stride + i) | sign << 31
+// per-window: key = w << (c - 1) | (|d| - 1), value = i | sign << 31
+template <class F>
+__device__ __forceinline__ void scalar_digits(const Fr &s, size_t i, const DigitArgs &A, F f) {
+  const Fr k = from_mont(s);
+  uint32_t carry = 0;
+  const int c = A.c;
+  const uint32_t half = 1u << (c - 1);
+  for (int w = 0; w < A.W; w++) {
+    const int bit = w * c;
+    const int limb = bit >> 5, sh = bit & 31;
+    const uint64_t lo = limb < 8 ? k.v[limb] : 0;
+    const uint64_t hi = limb + 1 < 8 ? k.v[limb + 1] : 0;
+    const uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1u << c) - 1));
+    const uint32_t val = raw + carry;
+    uint32_t neg = 0, mag;
+    if (val > half) {
+      mag = (1u << c) - val;
+      neg = 1;
+      carry = 1;
+    } else {
+      mag = val;
+      carry = 0;
+    }
+    if (mag) {
+      const uint32_t key = A.shared ? ((mag - 1) << A.wb) | (uint32_t)w : ((uint32_t)w << (c - 1)) | (mag - 1);
+      f(key, (uint32_t)(A.shared ? (size_t)w * A.stride + i : i) | (neg << 31));
+    }
+  }
+}
+
+// each thread's scalars of a pass-1 tile, BS_SCALARS loads in flight at a time
+template <class F>
+__device__ __forceinline__ void tile_scalars(const DigitArgs &A, size_t a, size_t b, F f) {
+  for (size_t i0 = a + threadIdx.x; i0 < b; i0 += (size_t)BS_SCALARS * BS_BLOCK) {
+    Fr s[BS_SCALARS];
+#pragma unroll
+    for (int j = 0; j < BS_SCALARS; j++) {
+      const size_t i = i0 + (size_t)j * BS_BLOCK;
+      if (i < b) s[j] = A.scalars[i];
+    }
+#pragma unroll
+    for (int j = 0; j < BS_SCALARS; j++) {
+      const size_t i = i0 + (size_t)j * BS_BLOCK;
+      if (i < b) scalar_digits(s[j], i, A, f);
+    }
+  }
+}
+
+// out[d] = sum_{d' < d} h[d'] for d < nb <= 2 * BS_BLOCK (two bins per thread)
+__device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out, int nb, uint32_t *wsum) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t h0 = 2 * t < nb ? h[2 * t] : 0u, h1 = 2 * t + 1 < nb ? h[2 * t + 1] : 0u;
+  const uint32_t mine = h0 + h1;
+  uint32_t x = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  uint32_t off = 0;
+  for (int i = 0; i < wv; i++) off += wsum[i];
+  const uint32_t ex = off + x - mine;
+  if (2 * t < nb) out[2 * t] = ex;
+  if (2 * t + 1 < nb) out[2 * t + 1] = ex + h0;
+  __syncthreads();
+}
+
+static_assert(BS_MAXBINS <= 2 * BS_BLOCK, "two bins per thread in the block scan");
+
+// Tile writer: entries already placed in lk/lv by bin (bin d at [lbase[d], lbase[d] + cnt));
+// consecutive lanes store consecutive slots of a bin's run at goff[d] + (slot - lbase[d]).
+template <class BinOf>
+__device__ __forceinline__ void write_tile(const uint32_t *lk, const uint32_t *lv, int m, const uint32_t *lbase,
+                                           const uint32_t *goff, BinOf bin, uint32_t *__restrict__ okeys,
+                                           uint32_t *__restrict__ ovals) {
+  for (int slot = threadIdx.x; slot < m; slot += BS_BLOCK) {
+    const uint32_t key = lk[slot];
+    const uint32_t d = bin(key);
+    const uint32_t pos = goff[d] + (uint32_t)slot - lbase[d];
+    okeys[pos] = key;
+    ovals[pos] = lv[slot];
+  }
+}
+
+// pass 1 histogram: counts[d * T1 + tile] = entries of the tile with top digit d
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_count1(DigitArgs A, int shift, int nbins, size_t T1,
+                                                        uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[BS_MAXBINS];
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h[d] = 0;
+  __syncthreads();
+  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  tile_scalars(A, a, b, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> shift], 1u); });
+  __syncthreads();
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) counts[(size_t)d * T1 + tile] = h[d];
+  if (tile == 0 && threadIdx.x == 0) counts[(size_t)nbins * T1] = 0;  // scan slot for the total
+}
+
+// pass 1 scatter: digits -> LDS ordered by bin -> coalesced runs
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift, int nbins, size_t T1,
+                                                          const uint32_t *__restrict__ offs,
+                                                          uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
+  __shared__ uint32_t lk[BS_TILE], lv[BS_TILE];
+  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
+    h[d] = 0;
+    goff[d] = offs[(size_t)d * T1 + tile];
+  }
+  __syncthreads();
+  tile_scalars(A, a, b, [&](uint32_t key, uint32_t) { atomicAdd(&h[key >> shift], 1u); });
+  __syncthreads();
+  block_scan_bins(h, lbase, nbins, wsum);
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h[d] = lbase[d];  // cursors
+  __syncthreads();
+  tile_scalars(A, a, b, [&](uint32_t key, uint32_t val) {  // second digit sweep (scalars are cached)
+    const uint32_t slot = atomicAdd(&h[key >> shift], 1u);
+    lk[slot] = key;
+    lv[slot] = val;
+  });
+  __syncthreads();
+  const int m = (int)h[nbins - 1];  // the last bin's cursor ends at the tile's entry count
+  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, keys, vals);
+}
+
+// bins of pass 1 -> segment starts; seg[nbins] = total = number of entries (also *valid)
+__global__ void k_bs_segs1(const uint32_t *__restrict__ offs, int nbins, size_t T1, uint32_t *__restrict__ seg,
+                           uint32_t *__restrict__ valid) {
+  for (int d = threadIdx.x; d <= nbins; d += blockDim.x) seg[d] = offs[(size_t)d * T1];
+  if (threadIdx.x == 0) *valid = offs[(size_t)nbins * T1];
+}
+
+// tiles per segment
+__global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t *__restrict__ tcount) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s <= S; s += (size_t)gridDim.x * blockDim.x)
+    tcount[s] = s < S ? (uint32_t)((seg[s + 1] - seg[s] + BS_TILE - 1) / BS_TILE) : 0u;
+}
+
+// desc[tile_base[s] + k] = s for the tiles k of segment s
+__global__ void k_bs_desc(const uint32_t *__restrict__ tbase, size_t S, uint32_t *__restrict__ desc) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < S; s += (size_t)gridDim.x * blockDim.x)
+    for (uint32_t g = tbase[s]; g < tbase[s + 1]; g++) desc[g] = (uint32_t)s;
+}
+
+struct PassGeom {
+  const uint32_t *seg, *tbase, *desc;
+  int shift, nbins;
+  uint32_t mask;
+};
+
+// passes >= 2, histogram: counts[nbins * tbase[s] + d * T_s + k]
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, size_t max_tiles,
+                                                       const uint32_t *__restrict__ keys, uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[BS_MAXBINS];
+  const size_t g = blockIdx.x;
+  if (g == max_tiles - 1 && threadIdx.x == 0) counts[(size_t)G.nbins * max_tiles] = 0;
+  if (g >= G.tbase[S]) {  // unused tile slot: zero its share of the scan input
+    for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * g + d] = 0;
+    return;
+  }
+  for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) h[d] = 0;
+  __syncthreads();
+  const uint32_t s = G.desc[g];
+  const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  const size_t a = G.seg[s] + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
+  uint32_t kk[BS_IPT];
+#pragma unroll
+  for (int j = 0; j < BS_IPT; j++) {
+    const size_t p = a + threadIdx.x + (size_t)j * BS_BLOCK;
+    kk[j] = p < e ? keys[p] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < BS_IPT; j++)
+    if (a + threadIdx.x + (size_t)j * BS_BLOCK < e) atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
+  __syncthreads();
+  for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + (size_t)d * Ts + k] = h[d];
+}
+
+// passes >= 2, scatter: tile -> LDS ordered by bin -> coalesced runs
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, const uint32_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ keys,
+                                                         const uint32_t *__restrict__ vals,
+                                                         uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals) {
+  __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
+  __shared__ uint32_t lk[BS_TILE], lv[BS_TILE];
+  const size_t g = blockIdx.x;
+  if (g >= G.tbase[S]) return;
+  const uint32_t s = G.desc[g];
+  const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) {
+    h[d] = 0;
+    goff[d] = offs[(size_t)G.nbins * tb + (size_t)d * Ts + k];
+  }
+  const size_t a = G.seg[s] + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
+  const int m = (int)(e - a);
+  uint32_t kk[BS_IPT], vv[BS_IPT], rk[BS_IPT];
+#pragma unroll
+  for (int j = 0; j < BS_IPT; j++) {
+    const int q = threadIdx.x + j * BS_BLOCK;
+    if (q < m) {
+      kk[j] = keys[a + q];
+      vv[j] = vals[a + q];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < BS_IPT; j++)
+    if ((int)threadIdx.x + j * BS_BLOCK < m) rk[j] = atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
+  __syncthreads();
+  block_scan_bins(h, lbase, G.nbins, wsum);
+#pragma unroll
+  for (int j = 0; j < BS_IPT; j++) {
+    if ((int)threadIdx.x + j * BS_BLOCK < m) {
+      const uint32_t slot = lbase[(kk[j] >> G.shift) & G.mask] + rk[j];
+      lk[slot] = kk[j];
+      lv[slot] = vv[j];
+    }
+  }
+  __syncthreads();
+  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return (key >> G.shift) & G.mask; }, okeys, ovals);
+}
+
+// new segments s * nbins + d: their starts; nseg[S * nbins] = end of the last segment
+__global__ void k_bs_segs(PassGeom G, size_t S, const uint32_t *__restrict__ offs, uint32_t *__restrict__ nseg) {
+  const size_t NS = S * (size_t)G.nbins;
+  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id <= NS; id += (size_t)gridDim.x * blockDim.x) {
+    if (id == NS) {
+      nseg[NS] = G.seg[S];
+      continue;
+    }
+    const size_t s = id / G.nbins, d = id % G.nbins;
+    const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb;
+    nseg[id] = Ts ? offs[(size_t)G.nbins * tb + d * Ts] : G.seg[s];
+  }
+}
+
+// bucket bounds from the (bucket, window) segment starts: out[b] = seg[b << wb], b <= nb
+__global__ void k_bs_bucket_starts(const uint32_t *__restrict__ seg, size_t nb, int wb, uint32_t *__restrict__ out) {
+  for (size_t b = blockIdx.x * (size_t)blockDim.x + threadIdx.x; b <= nb; b += (size_t)gridDim.x * blockDim.x)
+    out[b] = seg[b << wb];
+}
+
+template <class T>
+static void exclusive_scan(hipStream_t st, DevBuf &tmp, const T *in, T *out, size_t n) {
+  size_t bytes = 0;
+  TNS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, st));
+  void *t = tmp.ensure(bytes);
+  TNS_HIP(hipcub::DeviceScan::ExclusiveSum(t, bytes, in, out, (int)n, st));
+}
+
+// Groups the W*n digit entries of `scalars` by bucket (bucket_bits bits of bucket index;
+// per-window layout: window bits included).  Returns the key/value arrays holding the
+// result (two of the lane's four entry buffers), the bucket starts (bucket b =
+// [bstart[b], bstart[b+1]), b < 2^bucket_bits) and the shift from key to bucket;
+// *valid = number of entries (non-zero digits).
+BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+                            int bucket_bits, uint32_t *valid) {
+  hipStream_t st = ln.stream;
+  const size_t E = (size_t)W * n;
+  if (E >= ((size_t)1 << 32)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one bucket sort");
+  if (W > BS_TILE) throw Error(TNS_ERR_COMMITMENT, "too many MSM windows");
+  uint32_t *K[2] = {(uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * E), (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * E)};
+  uint32_t *V[2] = {(uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * E), (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * E)};
+  DigitArgs A{scalars, n, 0, c, W, 0, shared, stride};
+  if (shared)
+    while ((1 << A.wb) < W) A.wb++;
+  const int keybits = bucket_bits + A.wb;
+  const int npass = std::max(1, (keybits + BS_MAXBITS - 1) / BS_MAXBITS);
+  int bits[8] = {0};
+  bits[0] = keybits - BS_MAXBITS * (npass - 1);  // the smallest split first: pass-1 runs stay long
+  for (int p = 1; p < npass; p++) bits[p] = BS_MAXBITS;
+  int shift = keybits - bits[0];
+
+  // pass 1: scalars -> bins of the top bits[0] key bits
+  A.spb = (size_t)BS_TILE / W;
+  const size_t T1 = (n + A.spb - 1) / A.spb;
+  int nb = 1 << bits[0];
+  const size_t max_seg = (size_t)1 << keybits;
+  uint32_t *seg[2] = {(uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1)),
+                      (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1))};
+  const size_t max_tiles = (E + BS_TILE - 1) / BS_TILE + (max_seg >> bits[npass - 1]) + 1;
+  const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
+  uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
+  uint32_t *offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
+  k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+  TNS_LAUNCH_CHECK();
+  exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
+  k_bs_scatter1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  TNS_LAUNCH_CHECK();
+  k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
+  TNS_LAUNCH_CHECK();
+
+  size_t S = nb;
+  int cur = 0;
+  uint32_t *tcount = (uint32_t *)ln.ws[14].ensure(sizeof(uint32_t) * 2 * (max_seg + 1));
+  uint32_t *tbase = tcount + (max_seg + 1);
+  uint32_t *desc = (uint32_t *)ln.ws[15].ensure(sizeof(uint32_t) * max_tiles);
+  for (int p = 1; p < npass; p++) {
+    nb = 1 << bits[p];
+    shift -= bits[p];
+    const size_t tiles_bound = (E + BS_TILE - 1) / BS_TILE + S;
+    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, tcount);
+    TNS_LAUNCH_CHECK();
+    exclusive_scan(st, ln.ws[9], tcount, tbase, S + 1);
+    k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(tbase, S, desc);
+    TNS_LAUNCH_CHECK();
+    PassGeom G{seg[cur], tbase, desc, shift, nb, (uint32_t)nb - 1};
+    k_bs_count<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
+    TNS_LAUNCH_CHECK();
+    exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * tiles_bound + 1);
+    k_bs_scatter<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1], V[cur ^ 1]);
+    TNS_LAUNCH_CHECK();
+    k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, seg[cur ^ 1]);
+    TNS_LAUNCH_CHECK();
+    cur ^= 1;
+    S *= nb;
+  }
+  uint32_t *bstart = seg[cur];
+  if (A.wb) {  // (bucket, window) segments -> bucket starts
+    bstart = seg[cur ^ 1];
+    const size_t nbk = (size_t)1 << bucket_bits;
+    k_bs_bucket_starts<<<grid_for(nbk + 1, 256), 256, 0, st>>>(seg[cur], nbk, A.wb, bstart);
+    TNS_LAUNCH_CHECK();
+  }
+  return BucketOrder{K[cur], V[cur], bstart, A.wb};
+}
+
+}  // namespace tns

@@ -97,7 +97,7 @@ struct PinnedBuf {
 // (the two commitments, the two opening quotients) overlap on the device.
 struct MsmLane {
   hipStream_t stream = nullptr;
-  DevBuf ws[10];
+  DevBuf ws[16];
   DevBuf fix;       // heavy-bucket level sums
   PinnedBuf host;   // scalar bit length, then the per-set sums
 };
@@ -246,6 +246,15 @@ struct Ctx {
   std::map<std::tuple<size_t, size_t, size_t>, DevBuf *> bary_w;  // (N, first, count) -> weights
   bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
   bool msm_tables = true;                // shared-bucket MSM on fixed bases with window tables
+  // two-lane MSM schedule (TNS_MSM_STAGGER=1): lane 1 (high-priority stream) starts its sort
+  // only once lane 0's sort is done, so it runs under lane 0's accumulation.  Off by default:
+  // the accumulation is issue-bound, a co-running sort slows it by as much as it hides
+  // (C4: 63.6 ms/step staggered, 62.6 not)
+  bool msm_stagger = false;
+  bool msm_cub_sort = false;
+  // TNS_ACC_WAVES=k: k_accumulate as k resident 256-thread blocks per CU (grid-stride), leaving
+  // wave slots to a co-running sort; 0 (default) = one block per 256 chunks
+  int num_cu = 256, acc_waves = 0;  // rocPRIM radix sort of a digit array instead of bucket_sort_dev (A/B)
   KernelProfiler prof;
   ~Ctx();
 };
@@ -317,6 +326,13 @@ struct MsmArgs {
 };
 // two independent MSMs overlapped on the context's two lanes (inputs ready on c->stream)
 void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
+// bucket_sort.hip: the MSM's digit entries grouped by bucket (bucket k = [bstart[k], bstart[k+1]))
+struct BucketOrder {
+  uint32_t *keys, *vals, *bstart;
+  int ks;  // bucket = key >> ks
+};
+BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+                            int keybits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);
@@ -339,6 +355,10 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
                                Fr *ell_part, Fr *sum_part);
 // q_i = (v - y_i) * inv_i in place: the quotient's values on the slice
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
+void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
+                                Fr *inv, Fr parts[3]);
+void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
+                                   const Fr *inv, Fr *q0, Fr *q1);
 // quotient values for an opening AT the node j0 (value y_j0), unsharded
 void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q);
 bool fr_is_node(const Fr &x, size_t N);

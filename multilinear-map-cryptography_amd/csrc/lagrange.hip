@@ -49,18 +49,31 @@ __global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr
   cp[t] = acc;
 }
 
-// out[0] = prod_i in[i] (one block)
-__global__ void __launch_bounds__(1024) k_prod_reduce(const Fr *__restrict__ in, size_t n, Fr *__restrict__ out) {
-  __shared__ Fr lds[1024];
+// out[blockIdx.x] = prod of in[i] over the block's grid-stride share (one level of a product tree)
+__global__ void __launch_bounds__(256) k_prod_reduce(const Fr *__restrict__ in, size_t n, Fr *__restrict__ out) {
+  __shared__ Fr lds[256];
   Fr acc = Fr::one();
-  for (size_t i = threadIdx.x; i < n; i += blockDim.x) acc = mul(acc, in[i]);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    acc = mul(acc, in[i]);
   lds[threadIdx.x] = acc;
   __syncthreads();
   for (unsigned s = blockDim.x / 2; s > 0; s >>= 1) {
     if (threadIdx.x < s) lds[threadIdx.x] = mul(lds[threadIdx.x], lds[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[0] = lds[0];
+  if (threadIdx.x == 0) out[blockIdx.x] = lds[0];
+}
+
+// *out = prod_i in[i]: a 256-block level into tmp[0..256), then one block
+static void prod_reduce(hipStream_t st, const Fr *in, size_t n, Fr *tmp, Fr *out) {
+  if (n > 4096) {
+    k_prod_reduce<<<256, 256, 0, st>>>(in, n, tmp);
+    TNS_LAUNCH_CHECK();
+    in = tmp;
+    n = 256;
+  }
+  k_prod_reduce<<<1, 256, 0, st>>>(in, n, out);
+  TNS_LAUNCH_CHECK();
 }
 
 // Backward sweep of chain t: inv_i = 1/(x - i) from pre[i] and the chain inverse.
@@ -100,6 +113,48 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
     d = add(d, Tm);
   }
   if (!BASIS) sp[t] = s;
+}
+
+// k_node_finish<false> for two vectors on the same nodes: the inverses are shared.
+//   inv[i] = inv_i;  sp[t] = sum_chain w_i y0_i inv_i,  sp[T + t] = sum_chain w_i y1_i inv_i
+__global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
+                                                      const Fr *__restrict__ cp, const Fr *__restrict__ w,
+                                                      const Fr *__restrict__ y0, const Fr *__restrict__ y1,
+                                                      Fr *invs, Fr *__restrict__ sp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  if (t >= n) {
+    sp[t] = sp[T + t] = Fr::zero();
+    return;
+  }
+  const size_t cnt = (n - 1 - t) / T;
+  size_t i = t + cnt * T;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
+  Fr iv = inv(cp[t]);
+  Fr s0 = Fr::zero(), s1 = Fr::zero();
+  for (;;) {
+    const Fr inv_i = mul(iv, pre[i]);
+    iv = mul(iv, d);
+    invs[i] = inv_i;
+    const Fr wi = mul(w[i], inv_i);
+    s0 = add(s0, mul(wi, y0[i]));
+    s1 = add(s1, mul(wi, y1[i]));
+    if (i < T) break;
+    i -= T;
+    d = add(d, Tm);
+  }
+  sp[t] = s0;
+  sp[T + t] = s1;
+}
+
+// q0_i = (v0 - y0_i) inv_i, q1_i = (v1 - y1_i) inv_i; q1 may alias inv
+__global__ void __launch_bounds__(256) k_node_quotient2(const Fr *__restrict__ y0, const Fr *__restrict__ y1, Fr v0,
+                                                        Fr v1, size_t n, const Fr *invs, Fr *__restrict__ q0, Fr *q1) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const Fr iv = invs[i];
+    q0[i] = mul(sub(v0, y0[i]), iv);
+    q1[i] = mul(sub(v1, y1[i]), iv);
+  }
 }
 
 // q_i = (v - y_i) * inv_i, in place over inv
@@ -183,14 +238,13 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
-  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (2 * s.T + 4));
+  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (3 * s.T + 4 + 256));
   s.cp = ws;
-  s.sp = ws + s.T;
-  s.dev = ws + 2 * s.T;
+  s.sp = ws + s.T;  // 2T: room for two vectors' partial sums
+  s.dev = ws + 3 * s.T;
   k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp);
   TNS_LAUNCH_CHECK();
-  k_prod_reduce<<<1, 1024, 0, c->stream>>>(s.cp, s.T, s.dev);
-  TNS_LAUNCH_CHECK();
+  prod_reduce(c->stream, s.cp, s.T, s.dev + 4, s.dev);
   return s;
 }
 
@@ -211,8 +265,8 @@ const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t
   k_node_prod<<<grid_for(TG, 256, 1u << 30), 256, 0, c->stream>>>(srs.tau, N, TG, from_u64<FrCfg>((uint64_t)TG),
                                                                    ecp);
   TNS_LAUNCH_CHECK();
-  k_prod_reduce<<<1, 1024, 0, c->stream>>>(ecp, TG, ecp + TG);
-  TNS_LAUNCH_CHECK();
+  DevBuf tmpb;
+  prod_reduce(c->stream, ecp, TG, (Fr *)tmpb.ensure(sizeof(Fr) * 256), ecp + TG);
   DevBuf scal;
   Fr *sc = (Fr *)scal.ensure(sizeof(Fr) * cnt);  // pre, then canonical L_j(tau) in place
   const Fr xs = fr_shift(srs.tau, first);
@@ -276,6 +330,32 @@ void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q)
   const Fr qj0 = mul(h[1], inv(wj));
   TNS_HIP(hipMemcpyAsync(q + j0, &qj0, sizeof(Fr), hipMemcpyHostToDevice, c->stream));
   TNS_HIP(hipStreamSynchronize(c->stream));
+}
+
+// Two vectors on the same nodes, opened at the same z (Twist: addresses and values): one
+// batch inversion serves both.  parts = {ell, sum0, sum1}; inv receives the shared inverses.
+void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
+                                Fr *inv, Fr parts[3]) {
+  TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);  // pre write/read, inv write, y0, y1, w
+  const Fr *w = bary_weights(c, N, first, cnt);
+  const Fr xs = fr_shift(z, first);
+  NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
+  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.cp, w, y0, y1, inv,
+                                                                      s.sp);
+  TNS_LAUNCH_CHECK();
+  k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
+  TNS_LAUNCH_CHECK();
+  k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp + s.T, s.T, s.dev + 2);
+  TNS_LAUNCH_CHECK();
+  TNS_HIP(hipMemcpyAsync(parts, s.dev, 3 * sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+}
+
+void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
+                                   const Fr *inv, Fr *q0, Fr *q1) {
+  TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);
+  k_node_quotient2<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1);
+  TNS_LAUNCH_CHECK();
 }
 
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q) {

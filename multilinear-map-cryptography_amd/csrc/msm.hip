@@ -182,19 +182,20 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ end,
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
-                                                    HeadTail *__restrict__ ht, size_t nchunks) {
+                                                    HeadTail *__restrict__ ht, size_t nchunks, int ks) {
   const size_t valid = *valid_p;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
     const size_t a = t * ACC_K;
     if (a >= valid) continue;
     const size_t b = a + ACC_K < valid ? a + ACC_K : valid;
-    uint32_t cur = keys[a];
+    uint32_t cur = keys[a] >> ks;
     G1Xyzz acc = G1Xyzz::inf();
     for (size_t p = a;; p++) {
-      const uint32_t k = (p < b) ? keys[p] : 0xffffffffu;
+      const uint32_t k = (p < b) ? keys[p] >> ks : 0xffffffffu;
       if (k != cur) {  // flush the run of bucket `cur`
         const uint32_t s = start[cur], e = end[cur];
+        acc = xyzz_canon(acc);
         if (s < a) ht[t].head = acc;
         else if (e > b) ht[t].tail = acc;
         else buckets[cur] = acc;
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
         cur = k;
         acc = G1Xyzz::inf();
       }
-      acc = xyzz_madd(acc, load_signed_point(pts, vals[p]));
+      acc = xyzz_madd_lazy(acc, load_signed_point(pts, vals[p]));
     }
   }
 }
@@ -223,13 +224,13 @@ struct FixLevels {
 __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ keys,
                                                    const uint32_t *__restrict__ valid_p,
                                                    const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
-                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out) {
+                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks) {
   const size_t valid = *valid_p;
   for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < n_groups; g += (size_t)gridDim.x * blockDim.x) {
     size_t span = (size_t)ACC_K;
     for (int l = 0; l < level; l++) span *= FIX_FAN;
     const size_t a = g * span, b = a + span;  // entries covered
-    if (b > valid || keys[a] != keys[b - 1]) continue;
+    if (b > valid || (keys[a] >> ks) != (keys[b - 1] >> ks)) continue;
     G1Xyzz acc = level == 1 ? ht[g * FIX_FAN].head : below[g * FIX_FAN];
     for (int i = 1; i < FIX_FAN; i++)
       acc = xyzz_add(acc, level == 1 ? ht[g * FIX_FAN + i].head : below[g * FIX_FAN + i]);
@@ -466,8 +467,17 @@ static unsigned bits_result(MsmLane &ln) {
 }
 
 // Enqueue everything up to the per-set sums' readback on lane `ln` (asynchronous).
+// `sorted` (optional) is recorded on the lane once the sorted order exists (or right away
+// when there is no sort), so another lane can hold back its own sort until then.
 static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
-                       const FixedBase *fb, unsigned bits, MsmJob &J) {
+                       const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
+  struct Rec {
+    hipEvent_t e;
+    hipStream_t s;
+    ~Rec() {
+      if (e) (void)hipEventRecord(e, s);
+    }
+  } rec{sorted, ln.stream};
   J.lane = &ln;
   hipStream_t st = ln.stream;
   if (n == 0 || bits == 0) {  // all scalars zero
@@ -504,27 +514,37 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
-  uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
-  uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
-  uint32_t *keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
-  uint32_t *vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
-  uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
-  uint32_t *bstart = bounds, *bend = bounds + P.nb, *valid = bounds + 2 * P.nb;
-  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
   const size_t nchunks = (total + ACC_K - 1) / ACC_K;
-  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
-
-  {
-    TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
-    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
-                                               keys, vals);
-    TNS_LAUNCH_CHECK();
-  }
-  size_t temp_bytes = 0;
-  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total,
-                                             0, P.end_bit, st));
-  void *temp = ln.ws[9].ensure(temp_bytes);
-  {
+  uint32_t *keys2, *vals2, *bstart, *bend, *valid;
+  int ks = 0;  // bucket = key >> ks
+  if (!ctx->msm_cub_sort) {
+    TNS_PROF_ON(ctx, st, "msm_sort", 32.0 * n + 16.0 * total);
+    valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
+    const BucketOrder o = bucket_sort_dev(ln, scalars, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid);
+    keys2 = o.keys;
+    vals2 = o.vals;
+    bstart = o.bstart;
+    bend = o.bstart + 1;
+    ks = o.ks;
+  } else {
+    uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
+    uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
+    keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
+    vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
+    uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
+    bstart = bounds;
+    bend = bounds + P.nb;
+    valid = bounds + 2 * P.nb;
+    {
+      TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
+      k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
+                                                 keys, vals);
+      TNS_LAUNCH_CHECK();
+    }
+    size_t temp_bytes = 0;
+    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
+                                               P.end_bit, st));
+    void *temp = ln.ws[9].ensure(temp_bytes);
     TNS_PROF_ON(ctx, st, "msm_sort", 16.0 * total);
     TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
                                                P.end_bit, st));
@@ -532,10 +552,17 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
     k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
     TNS_LAUNCH_CHECK();
   }
+  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
+  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
+  if (rec.e) {
+    TNS_HIP(hipEventRecord(rec.e, st));
+    rec.e = nullptr;
+  }
   {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
-    k_accumulate<<<grid_for(nchunks, 256, 1u << 30), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
-                                                                   points, buckets, ht, nchunks);
+    const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
+    k_accumulate<<<grid_for(nchunks, 256, acc_cap), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
+                                                                   points, buckets, ht, nchunks, ks);
     TNS_LAUNCH_CHECK();
   }
   {
@@ -555,7 +582,7 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
         F.lv[l] = base + o;
         o += F.len[l];
         k_fix_level<<<grid_for(F.len[l], 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l, F.len[l],
-                                                                        F.lv[l]);
+                                                                        F.lv[l], ks);
         TNS_LAUNCH_CHECK();
       }
     }
@@ -645,7 +672,13 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
   MsmJob ja, jb;
-  msm_launch(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja);
+  hipEvent_t sorted = nullptr;
+  if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
+  msm_launch(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja, sorted);
+  if (sorted) {
+    TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
+    (void)hipEventDestroy(sorted);
+  }
   msm_launch(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
