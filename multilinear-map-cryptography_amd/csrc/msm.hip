@@ -19,7 +19,7 @@
 //     point index | sign<<31; zero digits get a sentinel key.
 //  2. rocPRIM/hipCUB radix sort of the (key, value) pairs by key.
 //  3. k_bucket_bounds: [start, end) of every bucket in the sorted order.
-//  4. k_accumulate: load-balanced -- each thread owns ACC_K consecutive sorted entries
+//  4. k_accumulate: load-balanced -- each thread owns acc_k consecutive sorted entries
 //     and XYZZ-madds the (possibly negated) affine points run by run; runs that cross a
 //     chunk boundary leave a head/tail partial; k_bucket_fixup completes those buckets (heavy buckets'
 //     chunk heads through FIX_FAN-ary level sums, so no thread walks a long run).
@@ -39,7 +39,6 @@
 
 namespace tns {
 
-constexpr int ACC_K = 32;  // sorted entries per accumulation thread
 constexpr int RED_L = 16;  // running-sum group size of the bucket reduction
 
 struct MsmPlan {
@@ -182,13 +181,14 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
                                                     const uint32_t *__restrict__ end,
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
-                                                    HeadTail *__restrict__ ht, size_t nchunks, int ks) {
+                                                    HeadTail *__restrict__ ht, size_t nchunks, int ks,
+                                                    int acc_k) {
   const size_t valid = *valid_p;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
-    const size_t a = t * ACC_K;
+    const size_t a = t * acc_k;
     if (a >= valid) continue;
-    const size_t b = a + ACC_K < valid ? a + ACC_K : valid;
+    const size_t b = a + acc_k < valid ? a + acc_k : valid;
     uint32_t cur = keys[a] >> ks;
     G1Xyzz acc = G1Xyzz::inf();
     for (size_t p = a;; p++) {
@@ -224,10 +224,11 @@ struct FixLevels {
 __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ keys,
                                                    const uint32_t *__restrict__ valid_p,
                                                    const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
-                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks) {
+                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks,
+                                                   int acc_k) {
   const size_t valid = *valid_p;
   for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < n_groups; g += (size_t)gridDim.x * blockDim.x) {
-    size_t span = (size_t)ACC_K;
+    size_t span = (size_t)acc_k;
     for (int l = 0; l < level; l++) span *= FIX_FAN;
     const size_t a = g * span, b = a + span;  // entries covered
     if (b > valid || (keys[a] >> ks) != (keys[b - 1] >> ks)) continue;
@@ -243,7 +244,7 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
 __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
                                                       const uint32_t *__restrict__ end,
                                                       const HeadTail *__restrict__ ht, FixLevels F,
-                                                      G1Xyzz *__restrict__ buckets, size_t nb) {
+                                                      G1Xyzz *__restrict__ buckets, size_t nb, int acc_k) {
   for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb;
        bk += (size_t)gridDim.x * blockDim.x) {
     const uint32_t s = start[bk], e = end[bk];
@@ -251,7 +252,7 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
       buckets[bk] = G1Xyzz::inf();
       continue;
     }
-    const size_t tf = s / ACC_K, tl = (e - 1) / ACC_K;
+    const size_t tf = s / acc_k, tl = (e - 1) / acc_k;
     if (tf == tl) continue;
     // one addition site: the items are head(tl), then the inner heads (tf, tl), peeled
     // to FIX_FAN-aligned ranges and climbing a level whenever both ends are aligned
@@ -450,6 +451,12 @@ struct MsmJob {
   bool tiny = false;       // k_msm_tiny path: one point in the lane's pinned buffer
   MsmPlan P;
   int L0 = 0, nbits = 0, specs = 0;
+  // between the sort phase and the accumulation phase
+  bool sorted = false;
+  const G1Affine *points = nullptr;
+  uint32_t *keys2 = nullptr, *vals2 = nullptr, *bstart = nullptr, *bend = nullptr, *valid = nullptr;
+  int ks = 0, acc_k = 0;
+  size_t nchunks = 0, n = 0;
 };
 
 static void bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
@@ -466,11 +473,11 @@ static unsigned bits_result(MsmLane &ln) {
   return *(unsigned *)ln.host.p;
 }
 
-// Enqueue everything up to the per-set sums' readback on lane `ln` (asynchronous).
-// `sorted` (optional) is recorded on the lane once the sorted order exists (or right away
-// when there is no sort), so another lane can hold back its own sort until then.
-static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
-                       const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
+// Phase 1 on lane `ln` (asynchronous): plan, digits and the bucket order.  Trivial cases
+// (all scalars zero, n <= 64) finish here.  `sorted` (optional) is recorded on the lane once
+// the bucket order exists (or right away when there is none).
+static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
+                            const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
   struct Rec {
     hipEvent_t e;
     hipStream_t s;
@@ -514,7 +521,8 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
-  const size_t nchunks = (total + ACC_K - 1) / ACC_K;
+  const int acc_k = ctx->acc_k;
+  const size_t nchunks = (total + acc_k - 1) / acc_k;
   uint32_t *keys2, *vals2, *bstart, *bend, *valid;
   int ks = 0;  // bucket = key >> ks
   if (!ctx->msm_cub_sort) {
@@ -552,17 +560,40 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
     k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
     TNS_LAUNCH_CHECK();
   }
-  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
-  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
   if (rec.e) {
     TNS_HIP(hipEventRecord(rec.e, st));
     rec.e = nullptr;
   }
+  J.sorted = true;
+  J.points = points;
+  J.keys2 = keys2;
+  J.vals2 = vals2;
+  J.bstart = bstart;
+  J.bend = bend;
+  J.valid = valid;
+  J.ks = ks;
+  J.acc_k = acc_k;
+  J.nchunks = nchunks;
+  J.n = n;
+}
+
+// Phase 2 (asynchronous): accumulation, bucket fixup, reduction and the per-set sums' readback.
+static void msm_launch_reduce(Ctx *ctx, MsmJob &J) {
+  if (!J.sorted) return;  // immediate / tiny: done in phase 1
+  MsmLane &ln = *J.lane;
+  hipStream_t st = ln.stream;
+  const MsmPlan &P = J.P;
+  const G1Affine *points = J.points;
+  uint32_t *keys2 = J.keys2, *vals2 = J.vals2, *bstart = J.bstart, *bend = J.bend, *valid = J.valid;
+  const int ks = J.ks, acc_k = J.acc_k;
+  const size_t nchunks = J.nchunks, n = J.n;
+  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
+  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
   {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
     k_accumulate<<<grid_for(nchunks, 256, acc_cap), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
-                                                                   points, buckets, ht, nchunks, ks);
+                                                                   points, buckets, ht, nchunks, ks, acc_k);
     TNS_LAUNCH_CHECK();
   }
   {
@@ -582,11 +613,11 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
         F.lv[l] = base + o;
         o += F.len[l];
         k_fix_level<<<grid_for(F.len[l], 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l, F.len[l],
-                                                                        F.lv[l], ks);
+                                                                        F.lv[l], ks, acc_k);
         TNS_LAUNCH_CHECK();
       }
     }
-    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb);
+    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb, acc_k);
     TNS_LAUNCH_CHECK();
   }
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
@@ -617,6 +648,13 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
     // the number of sorted non-zero digits = mixed additions of k_accumulate (profiling)
     TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   }
+}
+
+
+static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
+                       const FixedBase *fb, unsigned bits, MsmJob &J) {
+  msm_launch_sort(ctx, ln, points, scalars, n, fb, bits, J);
+  msm_launch_reduce(ctx, J);
 }
 
 // Wait for the lane and finish on the host: R = sum_g T_g + L0 * sum_b 2^b M_b per set,
@@ -672,14 +710,27 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
   MsmJob ja, jb;
-  hipEvent_t sorted = nullptr;
+  hipEvent_t sorted = nullptr, sa = nullptr, sb = nullptr;
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
-  msm_launch(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja, sorted);
-  if (sorted) {
+  TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
+  TNS_HIP(hipEventCreateWithFlags(&sb, hipEventDisableTiming));
+  msm_launch_sort(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja, sorted ? sorted : sa);
+  if (sorted) {  // staggered: lane 1 sorts under lane 0's accumulation
+    TNS_HIP(hipEventRecord(sa, l0.stream));
     TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
     (void)hipEventDestroy(sorted);
   }
-  msm_launch(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb);
+  msm_launch_sort(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb, sb);
+  if (!ctx->msm_stagger) {
+    // both (memory-bound) sorts first, then both accumulations: an accumulation launched
+    // while the other lane still sorts takes every slot and stalls that sort behind it
+    TNS_HIP(hipStreamWaitEvent(l0.stream, sb, 0));
+    TNS_HIP(hipStreamWaitEvent(l1.stream, sa, 0));
+  }
+  (void)hipEventDestroy(sa);
+  (void)hipEventDestroy(sb);
+  msm_launch_reduce(ctx, ja);
+  msm_launch_reduce(ctx, jb);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
 }
