@@ -251,11 +251,11 @@ struct Ctx {
   // the accumulation is issue-bound, a co-running sort slows it by as much as it hides
   // (C4: 63.6 ms/step staggered, 62.6 not)
   bool msm_stagger = false;
-  bool msm_cub_sort = false;
+  bool msm_cub_sort = false;  // TNS_MSM_SORT=cub: rocPRIM radix sort of a digit array (A/B)
   // TNS_ACC_WAVES=k: k_accumulate as k resident 256-thread blocks per CU (grid-stride), leaving
   // wave slots to a co-running sort; 0 (default) = one block per 256 chunks
   int num_cu = 256, acc_waves = 0;
-  int acc_k = 128;  // sorted entries per k_accumulate thread (TNS_ACC_K; C4: 32 -> 62.0, 128 -> 61.1 ms)  // rocPRIM radix sort of a digit array instead of bucket_sort_dev (A/B)
+  int acc_k = 128;  // sorted entries per k_accumulate thread (TNS_ACC_K; C4: 32 -> 62.0, 128 -> 61.1 ms)
   KernelProfiler prof;
   ~Ctx();
 };
