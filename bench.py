@@ -45,7 +45,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--log-ops", type=int, default=24, help="Twist trace length 2^k (C4: 24)")
     ap.add_argument("--no-extras", action="store_true", help="skip C2/C3 extras and the CPU baseline")
-    ap.add_argument("--cpu-baseline-ops", type=int, default=256, help="oracle sample size (C1: 256)")
+    ap.add_argument("--cpu-baseline-ops", type=int, default=256,
+                    help="reference-algorithm oracle sample size (C1: 256)")
+    ap.add_argument("--cpu-fast-log-ops", type=int, default=20,
+                    help="fast CPU baseline sample: one proof of 2^k operations (setup_params(18): k <= 20)")
     ap.add_argument("--commit-basis", choices=["lagrange", "coefficients"], default="lagrange",
                     help="prove via the setup's Lagrange-basis SRS (default) or via interpolation + "
                          "coefficient KZG (the reference's route); identical proofs")
@@ -140,7 +143,7 @@ def roofline_from_profile(ts, ctx):
     return roof, stages
 
 
-def cpu_baseline(n_ops):
+def cpu_reference_algorithms(n_ops):
     """The C oracle (reference algorithms: O(N^3) Lagrange, per-term commit, closure sum-check)."""
     from oracle import coracle as co
     from oracle import pyoracle as po
@@ -155,8 +158,49 @@ def cpu_baseline(n_ops):
     assert st == 0
     return {"value": round(n_ops / dt, 3), "unit": "ops/s", "cores": 1, "kind": "port",
             "sample": f"Twist::prove of the {n_ops}-op ProtocolBenchmarks trace (setup_params({L})) by the "
-                      f"single-threaded C oracle restating the reference algorithms; {dt:.2f} s",
-            "host_cpu": platform.processor() or platform.machine(), "host_nproc": os.cpu_count()}
+                      f"single-threaded C oracle restating the reference algorithms (O(N^3) interpolation); "
+                      f"{dt:.2f} s"}
+
+
+def host_threads():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the box's CPU share per GPU is 16 cores
+
+
+def cpu_baseline(ts, pp18, log_ops, gpu_check=True):
+    """Fast CPU baseline (SURVEY 8(d) 'fast-CPU'): oracle/fastcpu.c proves Twist with the GPU
+    path's algorithms (Lagrange-basis KZG, Pippenger MSM, fold sum-check) on host threads.
+    Bounded sample: one 2^log_ops-op proof of the src/benchmarks.rs:88-99 trace over
+    setup_params(18); the basis [L_j(tau)]G is the device-built setup artefact (downloaded,
+    not timed).  The proof is checked against the GPU's proof of the same trace."""
+    from oracle import coracle as co
+
+    n = 1 << log_ops
+    L = log_ops - 2
+    addr, val, isw = ts.bench_trace(1 << L, n)
+    lag = pp18.commitment_params.srs.lagrange_points(n)
+    w = co.bary_weights(n)
+    T = host_threads()
+    t0 = time.perf_counter()
+    st, proof = co.fast_twist_prove(lag, w, pp18.max_operations, addr, val, isw, T)
+    dt = time.perf_counter() - t0
+    assert st == 0
+    out = {"value": round(n / dt, 1), "unit": "ops/s", "cores": T, "kind": "port",
+           "sample": f"Twist::prove of a 2^{log_ops}-op trace (src/benchmarks.rs:88-99, setup_params(18)) with the "
+                     f"GPU path's algorithms in C (oracle/fastcpu.c: Lagrange-basis KZG, Pippenger MSM, fold "
+                     f"sum-check) on {T} host threads; {dt:.2f} s",
+           "host_cpu": platform.processor() or platform.machine(), "host_nproc": os.cpu_count()}
+    if gpu_check:
+        g = ts.Twist(pp18).prove_soa(addr, val, isw)
+        same = (g.address_commitment.commitment == proof["address_commitment"]
+                and g.value_commitment.commitment == proof["value_commitment"]
+                and [q.proof for q in g.opening_proofs] == proof["opening_proofs"]
+                and g.opening_point == proof["opening_point"])
+        out["proof_identical_to_gpu"] = bool(same)
+    return out
 
 
 def main():
@@ -275,7 +319,8 @@ def main():
         out["roofline"] = roof
         out["stages_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in stages.items()}
     if rank == 0 and world == 1 and not args.no_extras:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_baseline_ops)
+        out["cpu_baseline"] = cpu_baseline(ts, pp18, args.cpu_fast_log_ops)
+        out["cpu_reference_algorithms"] = cpu_reference_algorithms(args.cpu_baseline_ops)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if pg is not None:

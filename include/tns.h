@@ -118,6 +118,9 @@ int tns_srs_set_tau(tns_srs *srs, const uint64_t tau[4]);
  * proof of that size; part of setup, not of proving.  TNS_ERR_INVALID_PARAMETERS when
  * the SRS has no tau or N is not a power of two. */
 int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n);
+/* Copy that basis ([L_j(tau)]G, j < n; built if needed) to host memory (affine uint64_t[8]
+ * each): setup artefact for host-side provers (the CPU baseline of bench.py). */
+int tns_srs_lagrange_download(tns_ctx *ctx, tns_srs *srs, size_t n, uint64_t *g1_affine_out);
 /* Prove path selection: lagrange != 0 (default) commits/opens through the Lagrange
  * basis when the SRS has tau; 0 forces vector_to_polynomial + coefficient KZG
  * (src/twist.rs:151-163).  Both produce identical proofs. */

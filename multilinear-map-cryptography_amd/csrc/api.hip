@@ -449,6 +449,21 @@ int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n) {
   });
 }
 
+int tns_srs_lagrange_download(tns_ctx *ctx, tns_srs *srs, size_t n, uint64_t *g1_affine_out) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    if (!srs->s.has_tau) throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS has no tau");
+    if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
+    const bool saved = ctx->c.lagrange_commit;
+    ctx->c.lagrange_commit = true;
+    const LagrangeBasis *b = lagrange_basis_dev(&ctx->c, srs->s, n, 0, n);
+    ctx->c.lagrange_commit = saved;
+    if (!b) throw Error(TNS_ERR_INVALID_PARAMETERS, "tau is an interpolation node: no Lagrange basis");
+    TNS_HIP(hipMemcpy(g1_affine_out, b->points.p, sizeof(G1Affine) * n, hipMemcpyDeviceToHost));
+    return TNS_OK;
+  });
+}
+
 int tns_ctx_set_msm_tables(tns_ctx *ctx, int on) {
   return guarded([&]() {
     CtxScope g(&ctx->c);

@@ -185,6 +185,12 @@ class Srs:
         first proof of that size."""
         _check(N.load().tns_srs_prepare_lagrange(self.ctx.handle, self.handle, n))
 
+    def lagrange_points(self, n: int) -> np.ndarray:
+        """The Lagrange basis [L_j(tau)]G of the nodes 0..n-1 (affine limbs, host copy)."""
+        out = np.zeros((n, 8), dtype=np.uint64)
+        _check(N.load().tns_srs_lagrange_download(self.ctx.handle, self.handle, n, N.p64(out)))
+        return out
+
     def download(self, n: Optional[int] = None) -> np.ndarray:
         n = len(self) if n is None else n
         out = np.zeros((n, 8), dtype=np.uint64)

@@ -208,3 +208,33 @@ def horner(coeff_limbs, z_limbs):
     out = np.zeros(4, dtype=np.uint64)
     lib().orc_horner(_p(c), C.c_size_t(len(c)), _p(z), _p(out))
     return out
+
+
+# ----------------------------------------------------------------- fast CPU baseline (fastcpu.c)
+def bary_weights(N: int) -> np.ndarray:
+    w = np.zeros((N, 4), dtype=np.uint64)
+    lib().fc_bary_weights(C.c_size_t(N), _p(w))
+    return w
+
+
+def lagrange_basis(tau_limbs, N: int) -> np.ndarray:
+    """[L_j(tau)]G for the nodes 0..N-1 (affine limbs), by scalar multiplication: small N."""
+    t = np.ascontiguousarray(tau_limbs, dtype=np.uint64).reshape(4)
+    out = np.zeros((N, 8), dtype=np.uint64)
+    lib().fc_lagrange_basis(_p(t), C.c_size_t(N), _p(out))
+    return out
+
+
+def fast_twist_prove(lagrange, bary_w, max_ops, addr_u64, val_limbs, is_write, threads=1):
+    """Twist::prove with the GPU path's algorithms on `threads` host threads (fastcpu.c).
+    addr_u64: uint64 addresses, val_limbs: (n,4) Montgomery Fr, is_write: uint8."""
+    lag = np.ascontiguousarray(lagrange, dtype=np.uint64).reshape(-1, 8)
+    w = np.ascontiguousarray(bary_w, dtype=np.uint64).reshape(-1, 4)
+    a = np.ascontiguousarray(addr_u64, dtype=np.uint64)
+    v = np.ascontiguousarray(val_limbs, dtype=np.uint64).reshape(-1, 4)
+    isw = np.ascontiguousarray(is_write, dtype=np.uint8)
+    pr = OrcProof()
+    st = lib().fc_twist_prove(_p(lag), _p(w), C.c_size_t(len(lag)), C.c_size_t(max_ops), _p(a), _p(v),
+                              isw.ctypes.data_as(C.POINTER(C.c_uint8)), C.c_size_t(len(a)), C.c_int(threads),
+                              C.byref(pr))
+    return st, _proof_dict(pr, ("address_commitment", "value_commitment"))

@@ -1,0 +1,31 @@
+/*
+ * fastcpu.h -- the fast CPU baseline (fastcpu.c): Twist::prove with the MI355X path's
+ * algorithms on host threads.  BASELINE / TEST INFRASTRUCTURE ONLY (see oracle.h).
+ * Layouts as in oracle.h (uint64_t[4] Montgomery field elements, uint64_t[8] affine G1).
+ */
+#ifndef TNS_FASTCPU_H
+#define TNS_FASTCPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#include "oracle.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* barycentric weights w_j = (-1)^(N-1-j) / (j! (N-1-j)!) of the nodes 0..N-1 (N x 4) */
+void fc_bary_weights(size_t N, uint64_t *w);
+/* [L_j(tau)]G, j < N (N x 8), by scalar multiplication -- small N (tests) */
+void fc_lagrange_basis(const uint64_t tau[4], size_t N, uint64_t *out);
+/* Twist::prove of n_ops operations (N = next_pow2(n_ops) >= 2): addr as u64, val Montgomery
+ * Fr, is_write bytes; lagrange = [L_j(tau)]G and bary_w = fc_bary_weights(N).  threads: host
+ * threads to use.  Returns 0, 1 (InvalidParameters) or 2 (opening point on a node). */
+int fc_twist_prove(const uint64_t *lagrange, const uint64_t *bary_w, size_t N, size_t max_ops,
+                   const uint64_t *addr, const uint64_t *val, const uint8_t *is_write, size_t n_ops,
+                   int threads, orc_proof *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
