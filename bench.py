@@ -127,10 +127,11 @@ def roofline_from_profile(ts, ctx):
     roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic,
             "alg_bytes_per_launch": per_launch, "avg_launch_ms": round(avg_s * 1e3, 4),
-            "note": "dominant stage by device time; integer-VALU-bound (256-bit Montgomery), so the HBM "
-                    "fraction is low by construction (compute position: the 'compute' object); the two "
-                    "MSMs of each commit/open pair run concurrently on two streams, so a launch's duration "
-                    "includes its co-runner -- see DESIGN.md"}
+            "note": "dominant stage by device time: k_accumulate, averaged over a step's 4 launches (2 "
+                    "narrow-scalar commitments, 2 full-width openings); integer-VALU-bound (256-bit "
+                    "Montgomery), so the HBM fraction is low by construction (compute position: the "
+                    "'compute' object); the two MSMs of a commit/open pair accumulate one after the "
+                    "other, so each launch's HIP-event duration is its own kernel time -- see DESIGN.md"}
     ex = ts.profile_read_ex(ctx, "msm_accumulate")
     if ex["ops"] and ex["busy_ms"]:
         tmacs = ex["ops"] * MACS_PER_MADD / (ex["busy_ms"] / 1e3) / 1e12

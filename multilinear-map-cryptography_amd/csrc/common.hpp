@@ -181,6 +181,7 @@ struct KernelProfiler {
     for (auto &r : pending) {
       float ms = 0.f, t0 = 0.f, t1 = 0.f;
       if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+        if (getenv("TNS_PROF_DEBUG")) fprintf(stderr, "prof %s %.3f ms\n", r.name.c_str(), ms);
         auto &t = totals[r.name];
         t.ms += ms;
         t.launches += 1;
@@ -251,6 +252,7 @@ struct Ctx {
   // the accumulation is issue-bound, a co-running sort slows it by as much as it hides
   // (C4: 63.6 ms/step staggered, 62.6 not)
   bool msm_stagger = false;
+  bool msm_serial = true;    // TNS_MSM_SERIAL=0: let the two lanes' accumulations run together
   bool msm_cub_sort = false;  // TNS_MSM_SORT=cub: rocPRIM radix sort of a digit array (A/B)
   // TNS_ACC_WAVES=k: k_accumulate as k resident 256-thread blocks per CU (grid-stride), leaving
   // wave slots to a co-running sort; 0 (default) = one block per 256 chunks

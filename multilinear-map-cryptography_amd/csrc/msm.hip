@@ -578,8 +578,12 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
 }
 
 // Phase 2 (asynchronous): accumulation, bucket fixup, reduction and the per-set sums' readback.
-static void msm_launch_reduce(Ctx *ctx, MsmJob &J) {
-  if (!J.sorted) return;  // immediate / tiny: done in phase 1
+// `accumulated` (optional) is recorded on the lane right after the accumulation kernel.
+static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = nullptr) {
+  if (!J.sorted) {  // immediate / tiny: done in phase 1
+    if (accumulated) TNS_HIP(hipEventRecord(accumulated, J.lane->stream));
+    return;
+  }
   MsmLane &ln = *J.lane;
   hipStream_t st = ln.stream;
   const MsmPlan &P = J.P;
@@ -596,6 +600,7 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J) {
                                                                    points, buckets, ht, nchunks, ks, acc_k);
     TNS_LAUNCH_CHECK();
   }
+  if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
   {
     TNS_PROF_ON(ctx, st, "msm_fixup", 0.0);
     FixLevels F{};
@@ -729,7 +734,17 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   }
   (void)hipEventDestroy(sa);
   (void)hipEventDestroy(sb);
-  msm_launch_reduce(ctx, ja);
+  if (ctx->msm_serial) {
+    // the accumulations one after the other: each is VALU-bound on the whole chip, so run
+    // together they take as long, and each launch's own duration is then its kernel time
+    hipEvent_t acc_a;
+    TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+    msm_launch_reduce(ctx, ja, acc_a);
+    TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
+    (void)hipEventDestroy(acc_a);
+  } else {
+    msm_launch_reduce(ctx, ja);
+  }
   msm_launch_reduce(ctx, jb);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
