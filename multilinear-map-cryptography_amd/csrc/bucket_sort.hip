@@ -4,8 +4,8 @@
 // k_accumulate (msm.hip) needs the W*n (bucket, point|sign) entries of an MSM grouped by
 // bucket.  A general radix sort (rocPRIM onesweep) spends a digit kernel, a histogram pass
 // and one full read+write of keys and values per 8-bit digit on it.  Here:
-//  * pass 1 reads the SCALARS (32 B each, W entries per scalar), recomputes their digits in
-//    registers and scatters the entries straight into bins of the top key bits -- the
+//  * pass 1 reads the SCALARS (canonical form, written by msm.hip's k_scalar_bits; 32 B for W
+//    entries), recomputes their digits in registers and scatters the entries straight into bins of the top key bits -- the
 //    digit array never exists, and zero digits never enter the sort;
 //  * passes 2.. split each bin by the next key bits.  MSD order needs no stability, so a
 //    pass is per-tile LDS histograms + one exclusive scan + a scatter; tiles never cross a
@@ -49,15 +49,19 @@ struct DigitArgs {
 // per-window: key = w << (c - 1) | (|d| - 1), value = i | sign << 31
 template <class F>
 __device__ __forceinline__ void scalar_digits(const Fr &s, size_t i, const DigitArgs &A, F f) {
-  const Fr k = from_mont(s);
+  const Fr &k = s;  // canonical (k_scalar_bits wrote them)
   uint32_t carry = 0;
   const int c = A.c;
   const uint32_t half = 1u << (c - 1);
   for (int w = 0; w < A.W; w++) {
     const int bit = w * c;
     const int limb = bit >> 5, sh = bit & 31;
-    const uint64_t lo = limb < 8 ? k.v[limb] : 0;
-    const uint64_t hi = limb + 1 < 8 ? k.v[limb + 1] : 0;
+    uint64_t lo = 0, hi = 0;  // k.v[limb], k.v[limb + 1] by selects: a dynamic index would put
+#pragma unroll                // the scalars in scratch memory
+    for (int l = 0; l < 8; l++) {
+      lo = l == limb ? k.v[l] : lo;
+      hi = l == limb + 1 ? k.v[l] : hi;
+    }
     const uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1u << c) - 1));
     const uint32_t val = raw + carry;
     uint32_t neg = 0, mag;
@@ -211,6 +215,10 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
   __syncthreads();
   const uint32_t s = G.desc[g];
   const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  if (Ts == 1) {  // a one-tile segment: k_bs_scatter ranks it locally (no keys read here)
+    for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + d] = 0;
+    return;
+  }
   const size_t a = G.seg[s] + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
   uint32_t kk[BS_IPT];
 #pragma unroll
@@ -225,22 +233,28 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + (size_t)d * Ts + k] = h[d];
 }
 
-// passes >= 2, scatter: tile -> LDS ordered by bin -> coalesced runs
+// passes >= 2, scatter: tile -> LDS ordered by bin -> coalesced runs.  Segment s's block of
+// the scanned counts starts at offs[nbins tb]; one-tile segments (the common case in the last
+// pass) have zero counts there and take their bin offsets, and the next pass's segment
+// starts, from their own LDS scan.
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, const uint32_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ vals,
-                                                         uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals) {
+                                                         uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
+                                                         uint32_t *__restrict__ nseg) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   __shared__ uint32_t lk[BS_TILE], lv[BS_TILE];
   const size_t g = blockIdx.x;
   if (g >= G.tbase[S]) return;
   const uint32_t s = G.desc[g];
   const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  const uint32_t s0 = G.seg[s];
+  const uint32_t base = Ts == 1 ? 0u : s0 - offs[(size_t)G.nbins * tb];
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) {
     h[d] = 0;
-    goff[d] = offs[(size_t)G.nbins * tb + (size_t)d * Ts + k];
+    if (Ts != 1) goff[d] = base + offs[(size_t)G.nbins * tb + (size_t)d * Ts + k];
   }
-  const size_t a = G.seg[s] + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
+  const size_t a = s0 + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
   const int m = (int)(e - a);
   uint32_t kk[BS_IPT], vv[BS_IPT], rk[BS_IPT];
 #pragma unroll
@@ -257,6 +271,11 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     if ((int)threadIdx.x + j * BS_BLOCK < m) rk[j] = atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
   __syncthreads();
   block_scan_bins(h, lbase, G.nbins, wsum);
+  if (Ts == 1)
+    for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) {
+      goff[d] = s0 + lbase[d];
+      nseg[(size_t)s * G.nbins + d] = s0 + lbase[d];
+    }
 #pragma unroll
   for (int j = 0; j < BS_IPT; j++) {
     if ((int)threadIdx.x + j * BS_BLOCK < m) {
@@ -270,6 +289,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
 }
 
 // new segments s * nbins + d: their starts; nseg[S * nbins] = end of the last segment
+// (one-tile segments: written by k_bs_scatter)
 __global__ void k_bs_segs(PassGeom G, size_t S, const uint32_t *__restrict__ offs, uint32_t *__restrict__ nseg) {
   const size_t NS = S * (size_t)G.nbins;
   for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id <= NS; id += (size_t)gridDim.x * blockDim.x) {
@@ -279,7 +299,8 @@ __global__ void k_bs_segs(PassGeom G, size_t S, const uint32_t *__restrict__ off
     }
     const size_t s = id / G.nbins, d = id % G.nbins;
     const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb;
-    nseg[id] = Ts ? offs[(size_t)G.nbins * tb + d * Ts] : G.seg[s];
+    if (Ts == 1) continue;
+    nseg[id] = Ts ? G.seg[s] + (offs[(size_t)G.nbins * tb + d * Ts] - offs[(size_t)G.nbins * tb]) : G.seg[s];
   }
 }
 
@@ -357,7 +378,8 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
     k_bs_count<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * tiles_bound + 1);
-    k_bs_scatter<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1], V[cur ^ 1]);
+    k_bs_scatter<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1], V[cur ^ 1],
+                                                             seg[cur ^ 1]);
     TNS_LAUNCH_CHECK();
     k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, seg[cur ^ 1]);
     TNS_LAUNCH_CHECK();

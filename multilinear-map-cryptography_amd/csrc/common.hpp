@@ -97,7 +97,7 @@ struct PinnedBuf {
 // (the two commitments, the two opening quotients) overlap on the device.
 struct MsmLane {
   hipStream_t stream = nullptr;
-  DevBuf ws[16];
+  DevBuf ws[17];
   DevBuf fix;       // heavy-bucket level sums
   PinnedBuf host;   // scalar bit length, then the per-set sums
 };
@@ -257,7 +257,10 @@ struct Ctx {
   // TNS_ACC_WAVES=k: k_accumulate as k resident 256-thread blocks per CU (grid-stride), leaving
   // wave slots to a co-running sort; 0 (default) = one block per 256 chunks
   int num_cu = 256, acc_waves = 0;
-  int acc_k = 128;  // sorted entries per k_accumulate thread (TNS_ACC_K; C4: 32 -> 62.0, 128 -> 61.1 ms)
+  // sorted entries per k_accumulate thread (TNS_ACC_K fixes it; C4: 32 -> 62.0, 128 -> 61.1 ms).
+  // 0 = adaptive: 128, halved (down to 32) while the MSM would give fewer than acc_threads_cu
+  // threads per CU (small MSMs: enough waves per SIMD to hide the point gathers)
+  int acc_k = 0, acc_threads_cu = 1024;
   KernelProfiler prof;
   ~Ctx();
 };
@@ -334,7 +337,7 @@ struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
   int ks;  // bucket = key >> ks
 };
-BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
                             int keybits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)

@@ -96,12 +96,14 @@ static void finish_plan(MsmPlan &p) {
   p.nb = (size_t)p.Wr * p.half;
 }
 
-// *bits = max over i of bitlen(canonical scalar_i)
+// *bits = max over i of bitlen(canonical scalar_i); canon[i] = the canonical scalars (the
+// bucket sort's digit sweeps read these instead of converting the Montgomery form again)
 __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scalars, size_t n,
-                                                     unsigned *__restrict__ bits) {
+                                                     unsigned *__restrict__ bits, Fr *__restrict__ canon) {
   unsigned b = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr k = from_mont(scalars[i]);
+    canon[i] = k;
     for (int l = 7; l >= 0; l--)
       if (k.v[l]) {
         unsigned bl = 32 * l + 32 - __builtin_clz(k.v[l]);
@@ -303,22 +305,30 @@ __global__ void __launch_bounds__(64) k_reduce_level(const G1Xyzz *__restrict__ 
   }
 }
 
-// parts[(r specs + s) nch + ch] over the groups gi of chunk ch of set r:
-//   s < nbits: sum of S[gi] with bit s of gi set;  s == nbits: sum of T[gi]
+// parts[(r specs + s) nch + ch], nch = g / (2 CH) chunks of CH items per spec s of set r:
+//   s < nbits: the groups gi with bit s set, enumerated directly (the k-th is k with a one
+//   inserted at bit s: every lane of a wave adds, no masked-off lanes);
+//   s == nbits, nbits + 1: T over the lower / upper half of the groups
 __global__ void __launch_bounds__(64) k_masked_sums(const G1Xyzz *__restrict__ T, const G1Xyzz *__restrict__ S,
                                                     int sets, size_t g, int nbits, int CH,
                                                     G1Xyzz *__restrict__ parts) {
-  const int specs = nbits + 1;
-  const size_t nch = g / CH;
+  const int specs = nbits + 2;
+  const size_t nch = g / (2 * (size_t)CH);
   for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)sets * specs * nch;
        id += (size_t)gridDim.x * blockDim.x) {
     const size_t r = id / (specs * nch), rem = id % (specs * nch);
     const int sp = (int)(rem / nch);
     const size_t ch = rem % nch;
-    const G1Xyzz *src = (sp == nbits ? T : S) + r * g;
     G1Xyzz acc = G1Xyzz::inf();
-    for (size_t gi = ch * CH; gi < ch * CH + CH; gi++)
-      if (sp == nbits || ((gi >> sp) & 1)) acc = xyzz_add(acc, src[gi]);
+    if (sp >= nbits) {
+      const G1Xyzz *src = T + r * g + (size_t)(sp - nbits) * (g / 2);
+      for (size_t k = ch * CH; k < ch * CH + CH; k++) acc = xyzz_add(acc, src[k]);
+    } else {
+      const G1Xyzz *src = S + r * g;
+      const size_t lo_mask = ((size_t)1 << sp) - 1;
+      for (size_t k = ch * CH; k < ch * CH + CH; k++)
+        acc = xyzz_add(acc, src[((k & ~lo_mask) << 1) | ((size_t)1 << sp) | (k & lo_mask)]);
+    }
     parts[id] = acc;
   }
 }
@@ -459,13 +469,15 @@ struct MsmJob {
   size_t nchunks = 0, n = 0;
 };
 
-static void bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
+static const Fr *bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
+  Fr *canon = (Fr *)ln.ws[16].ensure(sizeof(Fr) * n);
   unsigned *d_bits = (unsigned *)ln.ws[4].ensure(sizeof(unsigned));
   unsigned *h_bits = (unsigned *)ln.host.ensure(sizeof(unsigned));
   TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), ln.stream));
-  k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits);
+  k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, canon);
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
+  return canon;
 }
 
 static unsigned bits_result(MsmLane &ln) {
@@ -476,8 +488,9 @@ static unsigned bits_result(MsmLane &ln) {
 // Phase 1 on lane `ln` (asynchronous): plan, digits and the bucket order.  Trivial cases
 // (all scalars zero, n <= 64) finish here.  `sorted` (optional) is recorded on the lane once
 // the bucket order exists (or right away when there is none).
-static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
-                            const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
+// canon: the canonical scalars from bits_launch (n > 64).
+static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
+                            size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
   struct Rec {
     hipEvent_t e;
     hipStream_t s;
@@ -521,14 +534,19 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
-  const int acc_k = ctx->acc_k;
+  int acc_k = ctx->acc_k;
+  if (acc_k <= 0) {
+    const size_t want = (size_t)ctx->num_cu * ctx->acc_threads_cu;
+    acc_k = 128;
+    while (acc_k > 32 && total / acc_k < want) acc_k /= 2;
+  }
   const size_t nchunks = (total + acc_k - 1) / acc_k;
   uint32_t *keys2, *vals2, *bstart, *bend, *valid;
   int ks = 0;  // bucket = key >> ks
   if (!ctx->msm_cub_sort) {
     TNS_PROF_ON(ctx, st, "msm_sort", 32.0 * n + 16.0 * total);
     valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
-    const BucketOrder o = bucket_sort_dev(ln, scalars, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid);
+    const BucketOrder o = bucket_sort_dev(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid);
     keys2 = o.keys;
     vals2 = o.vals;
     bstart = o.bstart;
@@ -627,20 +645,20 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
   }
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
   // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
-  // as nbits + 1 plain sums (the M_b and sum_g T_g) -- short dependency chains only
-  J.L0 = (int)std::min<size_t>(RED_L, P.half);
+  // as nbits + 2 plain sums (the M_b and sum_g T_g in two halves) -- short dependency chains only
+  J.L0 = (int)std::min<size_t>(RED_L, P.half / 2);  // c >= 4: half >= 8, so g >= 2
   const size_t g = P.half / J.L0;
   J.nbits = 0;
   while (((size_t)1 << J.nbits) < g) J.nbits++;
-  J.specs = J.nbits + 1;
+  J.specs = J.nbits + 2;
   {
     TNS_PROF_ON(ctx, st, "msm_reduce", 128.0 * P.nb);
     G1Xyzz *T = (G1Xyzz *)ln.ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * g);
     G1Xyzz *S = T + (size_t)P.Wr * g;
     k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
     TNS_LAUNCH_CHECK();
-    const int CH = (int)std::min<size_t>(16, g);
-    const size_t nch = g / CH;
+    const int CH = (int)std::min<size_t>(16, g / 2);
+    const size_t nch = g / (2 * (size_t)CH);
     const size_t nparts = (size_t)P.Wr * J.specs * nch;
     G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
     G1Xyzz *tmp = parts + nparts, *out = tmp + nparts;
@@ -656,9 +674,9 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
 }
 
 
-static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, size_t n,
-                       const FixedBase *fb, unsigned bits, MsmJob &J) {
-  msm_launch_sort(ctx, ln, points, scalars, n, fb, bits, J);
+static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
+                       size_t n, const FixedBase *fb, unsigned bits, MsmJob &J) {
+  msm_launch_sort(ctx, ln, points, scalars, canon, n, fb, bits, J);
   msm_launch_reduce(ctx, J);
 }
 
@@ -677,7 +695,7 @@ static G1Xyzz msm_complete(Ctx *ctx, MsmJob &J) {
     G1Xyzz acc = G1Xyzz::inf();
     for (int b = J.nbits - 1; b >= 0; b--) acc = xyzz_add(xyzz_dbl(acc), f[b]);
     for (int L = J.L0; L > 1; L >>= 1) acc = xyzz_dbl(acc);
-    Rw[r] = xyzz_add(f[J.nbits], acc);
+    Rw[r] = xyzz_add(xyzz_add(f[J.nbits], f[J.nbits + 1]), acc);
   }
   if (P.shared) return Rw[0];
   G1Xyzz acc = Rw[P.W - 1];
@@ -692,12 +710,13 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   if (n == 0) return G1Xyzz::inf();
   MsmLane &ln = ctx->lanes[0];
   unsigned bits = 254;
+  const Fr *canon = nullptr;
   if (n > 64) {
-    bits_launch(ln, scalars, n);
+    canon = bits_launch(ln, scalars, n);
     bits = bits_result(ln);
   }
   MsmJob J;
-  msm_launch(ctx, ln, points, scalars, n, fb, bits, J);
+  msm_launch(ctx, ln, points, scalars, canon, n, fb, bits, J);
   return msm_complete(ctx, J);
 }
 
@@ -710,8 +729,9 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   TNS_HIP(hipStreamWaitEvent(l1.stream, ready, 0));
   (void)hipEventDestroy(ready);
   unsigned ba = 254, bb = 254;
-  if (a.n > 64) bits_launch(l0, a.scalars, a.n);
-  if (b.n > 64) bits_launch(l1, b.scalars, b.n);
+  const Fr *ca = nullptr, *cb = nullptr;
+  if (a.n > 64) ca = bits_launch(l0, a.scalars, a.n);
+  if (b.n > 64) cb = bits_launch(l1, b.scalars, b.n);
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
   MsmJob ja, jb;
@@ -719,13 +739,13 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sb, hipEventDisableTiming));
-  msm_launch_sort(ctx, l0, a.points, a.scalars, a.n, a.fb, ba, ja, sorted ? sorted : sa);
+  msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sorted ? sorted : sa);
   if (sorted) {  // staggered: lane 1 sorts under lane 0's accumulation
     TNS_HIP(hipEventRecord(sa, l0.stream));
     TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
     (void)hipEventDestroy(sorted);
   }
-  msm_launch_sort(ctx, l1, b.points, b.scalars, b.n, b.fb, bb, jb, sb);
+  msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
   if (!ctx->msm_stagger) {
     // both (memory-bound) sorts first, then both accumulations: an accumulation launched
     // while the other lane still sorts takes every slot and stalls that sort behind it

@@ -1,0 +1,24 @@
+"""One full-width 2^k MSM over the SRS (fixed-base window tables), repeated: the sort /
+accumulate / reduction kernels without a second lane competing, for kernel traces.
+    rocprofv3 --kernel-trace --stats -d gpurun_out/msm -o run -- python3 tools/msm_trace.py 24
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "multilinear-map-cryptography_amd"))
+import twist_and_shout as ts  # noqa: E402
+
+k = int(sys.argv[1]) if len(sys.argv) > 1 else 24
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+pp, _ = ts.setup_params(k)
+ctx = ts.Context.get(0)
+n = 1 << k
+sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
+ref = ts.msm_resident(pp.commitment_params, sc, n)
+t = time.perf_counter()
+for _ in range(reps):
+    out = ts.msm_resident(pp.commitment_params, sc, n)
+    assert (out == ref).all()
+dt = (time.perf_counter() - t) / reps
+print(f"msm 2^{k}: {dt * 1e3:.3f} ms  {n / dt / 1e6:.1f} M pairs/s", flush=True)
