@@ -422,11 +422,11 @@ __device__ __forceinline__ G1Xyzz xyzz_madd_lazy(const G1Xyzz &p, const G1Affine
     if (fq_zero_lazy(R)) return xyzz_mdbl(q);
     return G1Xyzz::inf();
   }
-  const Fq PP = mul_lazy_dev(P, P);
+  const Fq PP = sqr_lazy_dev(P);
   const Fq PPP = mul_lazy_dev(P, PP);
   const Fq Q = mul_lazy_dev(p.x, PP);
   G1Xyzz r;
-  r.x = sub2_dev(sub2_dev(mul_lazy_dev(R, R), PPP), add2_dev(Q, Q));
+  r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
   r.y = sub2_dev(mul_lazy_dev(R, sub2_dev(Q, r.x)), mul_lazy_dev(p.y, PPP));
   r.zz = mul_lazy_dev(p.zz, PP);
   r.zzz = mul_lazy_dev(p.zzz, PPP);

@@ -23,6 +23,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 
@@ -31,14 +32,14 @@ namespace tns {
 constexpr int BS_BLOCK = 256;  // 4 waves: fits the slots k_accumulate leaves free
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
-constexpr int BS_TILE = 8192;  // entries per tile (LDS staging: 64 KiB)
-constexpr int BS_IPT = BS_TILE / BS_BLOCK;
+constexpr int BS_TILE = 8192;  // entries per tile at most (LDS staging: 64 KiB)
+// per-pass tile sizes (template parameter TILE of the scatter kernels): 8192 or 4096 entries
 constexpr int BS_SCALARS = 4;  // scalars a pass-1 thread loads ahead
 
 
 struct DigitArgs {
   const Fr *scalars;
-  size_t n, spb;  // scalars, scalars per tile (spb * W <= BS_TILE)
+  size_t n, spb;  // scalars, scalars per tile (spb * W <= TILE)
   int c, W, wb;   // window bits, windows, window-index bits appended to the key (shared)
   bool shared;
   uint32_t stride;
@@ -150,11 +151,12 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1(DigitArgs A, int shift, 
 }
 
 // pass 1 scatter: digits -> LDS ordered by bin -> coalesced runs
+template <int TILE>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift, int nbins, size_t T1,
                                                           const uint32_t *__restrict__ offs,
                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
-  __shared__ uint32_t lk[BS_TILE], lv[BS_TILE];
+  __shared__ uint32_t lk[TILE], lv[TILE];
   const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
     h[d] = 0;
@@ -184,9 +186,9 @@ __global__ void k_bs_segs1(const uint32_t *__restrict__ offs, int nbins, size_t 
 }
 
 // tiles per segment
-__global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t *__restrict__ tcount) {
+__global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t tile, uint32_t *__restrict__ tcount) {
   for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s <= S; s += (size_t)gridDim.x * blockDim.x)
-    tcount[s] = s < S ? (uint32_t)((seg[s + 1] - seg[s] + BS_TILE - 1) / BS_TILE) : 0u;
+    tcount[s] = s < S ? (uint32_t)((seg[s + 1] - seg[s] + tile - 1) / tile) : 0u;
 }
 
 // desc[tile_base[s] + k] = s for the tiles k of segment s
@@ -202,6 +204,7 @@ struct PassGeom {
 };
 
 // passes >= 2, histogram: counts[nbins * tbase[s] + d * T_s + k]
+template <int TILE>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, size_t max_tiles,
                                                        const uint32_t *__restrict__ keys, uint32_t *__restrict__ counts) {
   __shared__ uint32_t h[BS_MAXBINS];
@@ -219,15 +222,16 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
     for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + d] = 0;
     return;
   }
-  const size_t a = G.seg[s] + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
-  uint32_t kk[BS_IPT];
+  constexpr int IPT = TILE / BS_BLOCK;
+  const size_t a = G.seg[s] + (size_t)k * TILE, e = min((size_t)G.seg[s + 1], a + TILE);
+  uint32_t kk[IPT];
 #pragma unroll
-  for (int j = 0; j < BS_IPT; j++) {
+  for (int j = 0; j < IPT; j++) {
     const size_t p = a + threadIdx.x + (size_t)j * BS_BLOCK;
     kk[j] = p < e ? keys[p] : 0;
   }
 #pragma unroll
-  for (int j = 0; j < BS_IPT; j++)
+  for (int j = 0; j < IPT; j++)
     if (a + threadIdx.x + (size_t)j * BS_BLOCK < e) atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
   __syncthreads();
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + (size_t)d * Ts + k] = h[d];
@@ -237,13 +241,15 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
 // the scanned counts starts at offs[nbins tb]; one-tile segments (the common case in the last
 // pass) have zero counts there and take their bin offsets, and the next pass's segment
 // starts, from their own LDS scan.
+template <int TILE>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, const uint32_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ vals,
                                                          uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
                                                          uint32_t *__restrict__ nseg) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
-  __shared__ uint32_t lk[BS_TILE], lv[BS_TILE];
+  constexpr int IPT = TILE / BS_BLOCK;
+  __shared__ uint32_t lk[TILE], lv[TILE];
   const size_t g = blockIdx.x;
   if (g >= G.tbase[S]) return;
   const uint32_t s = G.desc[g];
@@ -254,11 +260,11 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     h[d] = 0;
     if (Ts != 1) goff[d] = base + offs[(size_t)G.nbins * tb + (size_t)d * Ts + k];
   }
-  const size_t a = s0 + (size_t)k * BS_TILE, e = min((size_t)G.seg[s + 1], a + BS_TILE);
+  const size_t a = s0 + (size_t)k * TILE, e = min((size_t)G.seg[s + 1], a + TILE);
   const int m = (int)(e - a);
-  uint32_t kk[BS_IPT], vv[BS_IPT], rk[BS_IPT];
+  uint32_t kk[IPT], vv[IPT], rk[IPT];
 #pragma unroll
-  for (int j = 0; j < BS_IPT; j++) {
+  for (int j = 0; j < IPT; j++) {
     const int q = threadIdx.x + j * BS_BLOCK;
     if (q < m) {
       kk[j] = keys[a + q];
@@ -267,7 +273,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < BS_IPT; j++)
+  for (int j = 0; j < IPT; j++)
     if ((int)threadIdx.x + j * BS_BLOCK < m) rk[j] = atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
   __syncthreads();
   block_scan_bins(h, lbase, G.nbins, wsum);
@@ -277,7 +283,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
       nseg[(size_t)s * G.nbins + d] = s0 + lbase[d];
     }
 #pragma unroll
-  for (int j = 0; j < BS_IPT; j++) {
+  for (int j = 0; j < IPT; j++) {
     if ((int)threadIdx.x + j * BS_BLOCK < m) {
       const uint32_t slot = lbase[(kk[j] >> G.shift) & G.mask] + rk[j];
       lk[slot] = kk[j];
@@ -318,6 +324,29 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const T *in, T *out, siz
   TNS_HIP(hipcub::DeviceScan::ExclusiveSum(t, bytes, in, out, (int)n, st));
 }
 
+// tile size of pass p (0-based; 8192 or 4096 entries).  TNS_BS_TILES="t0,t1,t2" overrides
+// (tuning); passes beyond the list use its last entry.
+static int pass_tile(int p) {
+  static int t[8] = {0};
+  static int nt = 0;
+  if (!nt) {
+    int def[3] = {8192, 8192, 8192};
+    for (int i = 0; i < 3; i++) t[i] = def[i];
+    nt = 3;
+    if (const char *e = getenv("TNS_BS_TILES")) {
+      int k = 0;
+      for (const char *q = e; *q && k < 8;) {
+        const int v = atoi(q);
+        t[k++] = v == 4096 ? 4096 : 8192;
+        while (*q && *q != ',') q++;
+        if (*q == ',') q++;
+      }
+      if (k) nt = k;
+    }
+  }
+  return t[p < nt ? p : nt - 1];
+}
+
 // Groups the W*n digit entries of `scalars` by bucket (bucket_bits bits of bucket index;
 // per-window layout: window bits included).  Returns the key/value arrays holding the
 // result (two of the lane's four entry buffers), the bucket starts (bucket b =
@@ -342,20 +371,22 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
-  A.spb = (size_t)BS_TILE / W;
+  const int tile1 = W <= 4096 ? pass_tile(0) : BS_TILE;
+  A.spb = (size_t)tile1 / W;
   const size_t T1 = (n + A.spb - 1) / A.spb;
   int nb = 1 << bits[0];
   const size_t max_seg = (size_t)1 << keybits;
   uint32_t *seg[2] = {(uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1)),
                       (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1))};
-  const size_t max_tiles = (E + BS_TILE - 1) / BS_TILE + (max_seg >> bits[npass - 1]) + 1;
+  const size_t max_tiles = (E + 4095) / 4096 + (max_seg >> bits[npass - 1]) + 1;  // smallest tile: 4096
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
   uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
   TNS_LAUNCH_CHECK();
   exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
-  k_bs_scatter1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  if (tile1 == 4096) k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  else k_bs_scatter1<BS_TILE><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
   TNS_LAUNCH_CHECK();
   k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
   TNS_LAUNCH_CHECK();
@@ -368,18 +399,24 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   for (int p = 1; p < npass; p++) {
     nb = 1 << bits[p];
     shift -= bits[p];
-    const size_t tiles_bound = (E + BS_TILE - 1) / BS_TILE + S;
-    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, tcount);
+    const int tile = pass_tile(p);
+    const size_t tiles_bound = (E + tile - 1) / tile + S;
+    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, (uint32_t)tile, tcount);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], tcount, tbase, S + 1);
     k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(tbase, S, desc);
     TNS_LAUNCH_CHECK();
     PassGeom G{seg[cur], tbase, desc, shift, nb, (uint32_t)nb - 1};
-    k_bs_count<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
+    if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
+    else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * tiles_bound + 1);
-    k_bs_scatter<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1], V[cur ^ 1],
-                                                             seg[cur ^ 1]);
+    if (tile == 4096)
+      k_bs_scatter<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1],
+                                                                     V[cur ^ 1], seg[cur ^ 1]);
+    else
+      k_bs_scatter<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1],
+                                                                        V[cur ^ 1], seg[cur ^ 1]);
     TNS_LAUNCH_CHECK();
     k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, seg[cur ^ 1]);
     TNS_LAUNCH_CHECK();

@@ -2,7 +2,7 @@
 // throughput on gfx950 for one build variant of the device arithmetic:
 //   -DTNS_MONT_MUL_INC='"<file>"'  product variant (default: csrc/mont_mul.inc)
 //   -DTNS_NO_FIELD_ASM             C add/sub/conditional subtraction instead of field_asm.inc
-// Built and run per variant by tools/maddbench.sh; prints one line.
+// Built here and run on the GPU box by tools/maddbench.sh; prints one line.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
