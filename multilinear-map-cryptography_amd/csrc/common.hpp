@@ -261,6 +261,7 @@ struct Ctx {
   // 0 = adaptive: 128, halved (down to 32) while the MSM would give fewer than acc_threads_cu
   // threads per CU (small MSMs: enough waves per SIMD to hide the point gathers)
   int acc_k = 0, acc_threads_cu = 1024;
+  int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
   KernelProfiler prof;
   ~Ctx();
 };

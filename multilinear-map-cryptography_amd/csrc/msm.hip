@@ -33,6 +33,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -399,7 +400,13 @@ __global__ void __launch_bounds__(256) k_dbl_times(G1Xyzz *__restrict__ x, size_
 }
 
 // the window a table for n points uses: the shared-layout optimum for full-width scalars
-static int table_window(size_t n) { return best_window(n, 254, 22, true); }
+static int table_window(size_t n) {
+  if (const char *e = getenv("TNS_TABLE_C")) {  // tuning: force the table window
+    const int c = atoi(e);
+    if (c >= 4 && c <= 22) return c;
+  }
+  return best_window(n, 254, 22, true);
+}
 
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n) {
   FixedBase *fb = new FixedBase();
@@ -646,7 +653,9 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
   // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
   // as nbits + 2 plain sums (the M_b and sum_g T_g in two halves) -- short dependency chains only
-  J.L0 = (int)std::min<size_t>(RED_L, P.half / 2);  // c >= 4: half >= 8, so g >= 2
+  // groups of L0 = 16 buckets (TNS_RED_L; 4 and 8 measured no faster at 2^20, 2 slower);
+  // c >= 4: half >= 8, so g >= 2
+  J.L0 = (int)std::min<size_t>(ctx->red_l > 0 ? ctx->red_l : RED_L, P.half / 2);
   const size_t g = P.half / J.L0;
   J.nbits = 0;
   while (((size_t)1 << J.nbits) < g) J.nbits++;
