@@ -18,7 +18,7 @@ STAGES = {
     "msm_sort": (["rocprim", "k_bucket_bounds", "k_bs_"], 4),
     "msm_accumulate": (["k_accumulate"], 4),
     "msm_fixup": (["k_fix_level", "k_bucket_fixup"], 4),
-    "msm_reduce": (["k_reduce_level", "k_sum_chunks", "k_set_sum"], 4),
+    "msm_reduce": (["k_reduce_level", "k_masked_sums", "k_sum_chunks", "k_set_sum"], 4),
     "open_scan": (["k_node_chain", "k_prod_reduce", "k_node_finish", "k_sum_reduce", "k_node_quotient"], 2),
     "sumcheck_round": (["k_sc_round", "k_sum_partials4"], None),
 }
