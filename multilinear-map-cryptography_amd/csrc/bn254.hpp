@@ -440,6 +440,33 @@ __device__ __forceinline__ G1Xyzz xyzz_canon(G1Xyzz p) {
   reduce_once_dev(p.zzz);
   return p;
 }
+
+// add-2008-s (XYZZ + XYZZ) in the lazy domain: both inputs in [0, 2M) (canonical points
+// included), result in [0, 2M); the identity is zz in {0, M}.  The bucket fixup and the
+// bucket reduction chain these; whatever the host reads goes through xyzz_canon first.
+__device__ __forceinline__ G1Xyzz xyzz_add_lazy(const G1Xyzz &p, const G1Xyzz &q) {
+  if (fq_zero_lazy(q.zz)) return p;
+  if (fq_zero_lazy(p.zz)) return q;
+  const Fq U1 = mul_lazy_dev(p.x, q.zz);
+  const Fq U2 = mul_lazy_dev(q.x, p.zz);
+  const Fq S1 = mul_lazy_dev(p.y, q.zzz);
+  const Fq S2 = mul_lazy_dev(q.y, p.zzz);
+  const Fq P = sub2_dev(U2, U1);
+  const Fq R = sub2_dev(S2, S1);
+  if (fq_zero_lazy(P)) {
+    if (fq_zero_lazy(R)) return xyzz_dbl(xyzz_canon(p));
+    return G1Xyzz::inf();
+  }
+  const Fq PP = sqr_lazy_dev(P);
+  const Fq PPP = mul_lazy_dev(P, PP);
+  const Fq Q = mul_lazy_dev(U1, PP);
+  G1Xyzz r;
+  r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
+  r.y = sub2_dev(mul_lazy_dev(R, sub2_dev(Q, r.x)), mul_lazy_dev(S1, PPP));
+  r.zz = mul_lazy_dev(mul_lazy_dev(p.zz, q.zz), PP);
+  r.zzz = mul_lazy_dev(mul_lazy_dev(p.zzz, q.zzz), PPP);
+  return r;
+}
 #endif
 
 // add-2008-s: XYZZ + XYZZ

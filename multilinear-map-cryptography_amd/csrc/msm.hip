@@ -237,7 +237,7 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
     if (b > valid || (keys[a] >> ks) != (keys[b - 1] >> ks)) continue;
     G1Xyzz acc = level == 1 ? ht[g * FIX_FAN].head : below[g * FIX_FAN];
     for (int i = 1; i < FIX_FAN; i++)
-      acc = xyzz_add(acc, level == 1 ? ht[g * FIX_FAN + i].head : below[g * FIX_FAN + i]);
+      acc = xyzz_add_lazy(acc, level == 1 ? ht[g * FIX_FAN + i].head : below[g * FIX_FAN + i]);
     out[g] = acc;
   }
 }
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
         else i = --hi;  // lo aligned, hi not
         item = l == 0 ? &ht[i].head : &F.lv[l][i];
       }
-      acc = xyzz_add(acc, *item);
+      acc = xyzz_add_lazy(acc, *item);
     }
     buckets[bk] = acc;
   }
@@ -298,8 +298,8 @@ __global__ void __launch_bounds__(64) k_reduce_level(const G1Xyzz *__restrict__ 
     const G1Xyzz *x = X + r * n + g * L;
     G1Xyzz run = G1Xyzz::inf(), acc = G1Xyzz::inf();
     for (int j = L - 1; j >= 0; j--) {
-      run = xyzz_add(run, x[j]);
-      acc = xyzz_add(acc, run);
+      run = xyzz_add_lazy(run, x[j]);
+      acc = xyzz_add_lazy(acc, run);
     }
     T[id] = acc;
     S[id] = run;
@@ -323,12 +323,12 @@ __global__ void __launch_bounds__(64) k_masked_sums(const G1Xyzz *__restrict__ T
     G1Xyzz acc = G1Xyzz::inf();
     if (sp >= nbits) {
       const G1Xyzz *src = T + r * g + (size_t)(sp - nbits) * (g / 2);
-      for (size_t k = ch * CH; k < ch * CH + CH; k++) acc = xyzz_add(acc, src[k]);
+      for (size_t k = ch * CH; k < ch * CH + CH; k++) acc = xyzz_add_lazy(acc, src[k]);
     } else {
       const G1Xyzz *src = S + r * g;
       const size_t lo_mask = ((size_t)1 << sp) - 1;
       for (size_t k = ch * CH; k < ch * CH + CH; k++)
-        acc = xyzz_add(acc, src[((k & ~lo_mask) << 1) | ((size_t)1 << sp) | (k & lo_mask)]);
+        acc = xyzz_add_lazy(acc, src[((k & ~lo_mask) << 1) | ((size_t)1 << sp) | (k & lo_mask)]);
     }
     parts[id] = acc;
   }
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(64) k_sum_chunks(const G1Xyzz *__restrict__ in
                                                    G1Xyzz *__restrict__ out) {
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n_out; t += (size_t)gridDim.x * blockDim.x) {
     G1Xyzz acc = in[t * chunk];
-    for (int i = 1; i < chunk; i++) acc = xyzz_add(acc, in[t * chunk + i]);
+    for (int i = 1; i < chunk; i++) acc = xyzz_add_lazy(acc, in[t * chunk + i]);
     out[t] = acc;
   }
 }
@@ -350,14 +350,14 @@ __global__ void __launch_bounds__(256) k_set_sum(const G1Xyzz *__restrict__ part
   __shared__ G1Xyzz lds[256];
   const size_t r = blockIdx.x;
   G1Xyzz acc = G1Xyzz::inf();
-  for (size_t g = threadIdx.x; g < groups; g += blockDim.x) acc = xyzz_add(acc, parts[r * groups + g]);
+  for (size_t g = threadIdx.x; g < groups; g += blockDim.x) acc = xyzz_add_lazy(acc, parts[r * groups + g]);
   lds[threadIdx.x] = acc;
   __syncthreads();
   for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) lds[threadIdx.x] = xyzz_add(lds[threadIdx.x], lds[threadIdx.x + s]);
+    if ((int)threadIdx.x < s) lds[threadIdx.x] = xyzz_add_lazy(lds[threadIdx.x], lds[threadIdx.x + s]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[r] = lds[0];
+  if (threadIdx.x == 0) out[r] = xyzz_canon(lds[0]);  // the host reads canonical coordinates
 }
 
 // Naive path for tiny inputs: one thread per point, double-and-add, then a tree.
