@@ -262,6 +262,7 @@ struct Ctx {
   // threads per CU (small MSMs: enough waves per SIMD to hide the point gathers)
   int acc_k = 0, acc_threads_cu = 1024;
   int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
+  int red_ch = 0;  // masked-sum chunk length (TNS_RED_CH, power of two; 0 = 16)
   KernelProfiler prof;
   ~Ctx();
 };

@@ -655,7 +655,10 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
   // as nbits + 2 plain sums (the M_b and sum_g T_g in two halves) -- short dependency chains only
   // groups of L0 = 16 buckets (TNS_RED_L; 4 and 8 measured no faster at 2^20, 2 slower);
   // c >= 4: half >= 8, so g >= 2
-  J.L0 = (int)std::min<size_t>(ctx->red_l > 0 ? ctx->red_l : RED_L, P.half / 2);
+  // up to 2^19 buckets per set the chains are the latency: groups of 4 and masked-sum chunks of 8
+  // (C2, 2^20 points: 2.73 -> 2.65 ms); from 2^21 buckets 16 / 16 stay the fastest (2^22, 2^24)
+  const bool small_sets = P.half <= ((size_t)1 << 19);
+  J.L0 = (int)std::min<size_t>(ctx->red_l > 0 ? ctx->red_l : (small_sets ? 4 : RED_L), P.half / 2);
   const size_t g = P.half / J.L0;
   J.nbits = 0;
   while (((size_t)1 << J.nbits) < g) J.nbits++;
@@ -666,7 +669,7 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
     G1Xyzz *S = T + (size_t)P.Wr * g;
     k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
     TNS_LAUNCH_CHECK();
-    const int CH = (int)std::min<size_t>(16, g / 2);
+    const int CH = (int)std::min<size_t>(ctx->red_ch > 0 ? ctx->red_ch : (small_sets ? 8 : 16), g / 2);
     const size_t nch = g / (2 * (size_t)CH);
     const size_t nparts = (size_t)P.Wr * J.specs * nch;
     G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
