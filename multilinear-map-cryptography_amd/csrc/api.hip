@@ -45,8 +45,6 @@ Ctx::~Ctx() {
   for (auto &kv : pass_tw) delete kv.second;
   for (auto &kv : bary_w) delete kv.second;
   if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
-  if (mask_sort) (void)hipStreamDestroy(mask_sort);
-  if (mask_acc) (void)hipStreamDestroy(mask_acc);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -329,22 +327,6 @@ int tns_ctx_create(int device, tns_ctx **out) {
     x->c.msm_cub_sort = cs && std::string(cs) == "cub";
     TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking,
                                         x->c.msm_stagger ? prio_hi : prio_lo));
-    if (const char *sc = getenv("TNS_SORT_CUS")) x->c.sort_cus = std::max(0, atoi(sc));
-    if (x->c.sort_cus > 0 && x->c.sort_cus < x->c.num_cu) {
-      // the sort's CUs spread evenly over the CU index space (so over the XCDs)
-      const int ncu = x->c.num_cu, k = x->c.sort_cus, words = (ncu + 31) / 32;
-      std::vector<uint32_t> ms(words, 0u), ma(words, 0u);
-      int picked = 0;
-      for (int i = 0; i < ncu; i++) {
-        const bool sort_cu = picked < k && (long)i * k / ncu == picked && (long)i * k % ncu < k;
-        if (sort_cu) picked++;
-        (sort_cu ? ms : ma)[i / 32] |= 1u << (i % 32);
-      }
-      TNS_HIP(hipExtStreamCreateWithCUMask(&x->c.mask_sort, (uint32_t)words, ms.data()));
-      TNS_HIP(hipExtStreamCreateWithCUMask(&x->c.mask_acc, (uint32_t)words, ma.data()));
-    } else {
-      x->c.sort_cus = 0;
-    }
     *out = x;
     return TNS_OK;
   });

@@ -263,12 +263,6 @@ struct Ctx {
   int acc_k = 0, acc_threads_cu = 1024;
   int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
   int red_ch = 0;  // masked-sum chunk length (TNS_RED_CH, power of two; 0 = 16)
-  // TNS_SORT_CUS=k: split the CUs for an MSM pair -- lane 1's bucket sort runs on k CUs
-  // (mask_sort) while lane 0's accumulation runs on the rest (mask_acc), after lane 0's own
-  // sort had the whole chip.  A sort sharing CUs with the accumulation waits for wave slots
-  // the accumulation never frees; on CUs of its own it runs under it.  0 = off.
-  int sort_cus = 0;
-  hipStream_t mask_sort = nullptr, mask_acc = nullptr;
   KernelProfiler prof;
   ~Ctx();
 };

@@ -747,38 +747,6 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
   MsmJob ja, jb;
-  if (ctx->sort_cus > 0) {
-    // split schedule: lane 0 sorts on the whole chip; then lane 1 sorts on the sort CUs while
-    // lane 0 accumulates (and reduces) on the others; then lane 1 accumulates on the whole chip
-    auto ev = [](hipStream_t from, hipStream_t to) {  // `to` waits for `from`'s work so far
-      hipEvent_t e;
-      TNS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      TNS_HIP(hipEventRecord(e, from));
-      TNS_HIP(hipStreamWaitEvent(to, e, 0));
-      (void)hipEventDestroy(e);
-    };
-    const hipStream_t s0 = l0.stream, s1 = l1.stream;
-    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja);
-    ev(s0, ctx->mask_sort);
-    ev(s1, ctx->mask_sort);
-    l1.stream = ctx->mask_sort;
-    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb);
-    l1.stream = s1;
-    ev(ctx->mask_sort, s1);
-    ev(s0, ctx->mask_acc);
-    hipEvent_t acc_a;
-    TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
-    l0.stream = ctx->mask_acc;
-    msm_launch_reduce(ctx, ja, acc_a);
-    l0.stream = s0;
-    ev(ctx->mask_acc, s0);
-    TNS_HIP(hipStreamWaitEvent(s1, acc_a, 0));  // the accumulations one after the other
-    (void)hipEventDestroy(acc_a);
-    msm_launch_reduce(ctx, jb);
-    out[0] = msm_complete(ctx, ja);
-    out[1] = msm_complete(ctx, jb);
-    return;
-  }
   hipEvent_t sorted = nullptr, sa = nullptr, sb = nullptr;
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
