@@ -526,6 +526,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   MsmPlan &P = J.P;
   P = MsmPlan();
   P.c = best_window(n, (int)bits, 20, false);
+  if (ctx->msm_c >= 4) P.c = ctx->msm_c;
   P.W = windows_for((int)bits, P.c);
   if (fb && ctx->msm_tables && fb->n >= n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
     const int Ws = windows_for((int)bits, fb->c);
