@@ -322,6 +322,7 @@ int tns_ctx_create(int device, tns_ctx **out) {
     if (const char *at = getenv("TNS_ACC_THREADS_CU")) x->c.acc_threads_cu = std::max(1, atoi(at));
     if (const char *rl = getenv("TNS_RED_L")) x->c.red_l = std::max(0, atoi(rl));
     if (const char *rc = getenv("TNS_RED_CH")) x->c.red_ch = std::max(0, atoi(rc));
+    if (const char *sc = getenv("TNS_SC_TAIL")) x->c.sc_tail = sc[0] != '0';
     if (const char *mc = getenv("TNS_MSM_C")) x->c.msm_c = std::max(0, std::min(20, atoi(mc)));
     if (const char *se = getenv("TNS_MSM_SERIAL")) x->c.msm_serial = se[0] != '0';
     const char *cs = getenv("TNS_MSM_SORT");

@@ -263,6 +263,7 @@ struct Ctx {
   int acc_k = 0, acc_threads_cu = 1024;
   int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
   int red_ch = 0;  // masked-sum chunk length (TNS_RED_CH, power of two; 0 = 16)
+  bool sc_tail = true;  // TNS_SC_TAIL=0: closure-free sum-check folds its last rounds launch by launch (A/B)
   int msm_c = 0;   // TNS_MSM_C=c: per-window bucket width for the generic-base layout (A/B; 0 = cost model)
   KernelProfiler prof;
   ~Ctx();

@@ -192,6 +192,36 @@ __global__ void __launch_bounds__(256) k_sum_partials4(const Fr *__restrict__ pa
     for (int x = 0; x < 4; x++) out[x] = acc[x];
 }
 
+// Closure-free sum-check (no composition terms: every round polynomial is zero, so the
+// challenges never wait for the device): the last m folds of the chain in one workgroup.
+// Tables of 2^m entries in a[]; fold j binds ch[j] (LSB first, as k_sc_round) and ping-pongs
+// a -> b -> a ...; out[i] = table i bound at all m challenges.  Replaces m - 1 small
+// k_sc_round launches and the k final k_mle_fold launches (each ~20 us of launch gap).
+struct ScTail {
+  Fr *a[MAX_SC_TABLES];
+  Fr *b[MAX_SC_TABLES];
+};
+constexpr unsigned SC_TAIL_LOG = 12;  // tables of <= 2^12 entries fold in the tail kernel
+
+__global__ void __launch_bounds__(1024) k_sc_fold_tail(ScTail t, int k, int m, const Fr *__restrict__ ch,
+                                                       Fr *__restrict__ out) {
+  for (int j = 0; j < m; j++) {
+    const Fr r = ch[j];
+    const unsigned half = 1u << (m - 1 - j);
+    for (int i = 0; i < k; i++) {
+      const Fr *in = (j & 1) ? t.b[i] : t.a[i];
+      Fr *o = (j & 1) ? t.a[i] : t.b[i];
+      for (unsigned s = threadIdx.x; s < half; s += blockDim.x) {
+        const Fr x0 = in[2 * s], x1 = in[2 * s + 1];
+        o[s] = add(x0, mul(r, sub(x1, x0)));
+      }
+    }
+    __syncthreads();  // fold j's outputs are fold j+1's inputs (other threads' entries)
+  }
+  if (threadIdx.x == 0)
+    for (int i = 0; i < k; i++) out[i] = ((m & 1) ? t.b[i] : t.a[i])[0];
+}
+
 static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n_terms) {
   Fr s = Fr::zero();
   for (int t = 0; t < n_terms; t++) {
@@ -226,7 +256,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   Fr *bufB[MAX_SC_TABLES];
   for (int i = 0; i < k; i++) bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
   const int nblk = (int)grid_for(n / 2 + 1, 256, 2048);
-  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * 4 * (size_t)nblk);
+  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * (size_t)nblk, 64));
   Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
 
   Fr cur = claimed;
@@ -237,27 +267,36 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   }
   Fr r_prev = Fr::zero();
   char lab[64];
+  // closure-free chains hand their last folds to k_sc_fold_tail: from round `tail_rnd` on
+  // (input tables of n >> (tail_rnd - 1) <= 2^SC_TAIL_LOG entries) only the transcript runs
+  const unsigned tail_rnd =
+      (c->sc_tail && !has_terms && k > 0 && nv >= 2) ? std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG)) : nv + 1;
+  Fr tail_ch[64];
   for (unsigned rnd = 0; rnd < nv; rnd++) {
     const size_t P = n >> (rnd + 1);  // output pairs of this round
-    ScTables tt{};
-    for (int i = 0; i < k; i++) {
-      tt.in[i] = src[i];
-      tt.out[i] = dst[i];
-    }
     const unsigned g = grid_for(P, 256, 2048);
-    TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
-    if (rnd == 0) {
-      if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+    if (rnd >= tail_rnd) {
+      tail_ch[rnd - tail_rnd] = r_prev;  // this round's fold runs in k_sc_fold_tail
     } else {
-      if (has_terms)
-        k_sc_round<true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-      else
-        k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-      // src now holds the freshly folded 2P-entry tables; the caller's tables
-      // become the next destination (they are consumed).
-      for (int i = 0; i < k; i++) std::swap(src[i], dst[i]);
+      ScTables tt{};
+      for (int i = 0; i < k; i++) {
+        tt.in[i] = src[i];
+        tt.out[i] = dst[i];
+      }
+      TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
+      if (rnd == 0) {
+        if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+      } else {
+        if (has_terms)
+          k_sc_round<true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+        else
+          k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+        // src now holds the freshly folded 2P-entry tables; the caller's tables
+        // become the next destination (they are consumed).
+        for (int i = 0; i < k; i++) std::swap(src[i], dst[i]);
+      }
+      TNS_LAUNCH_CHECK();
     }
-    TNS_LAUNCH_CHECK();
     Fr e[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
     if (has_terms) {
       k_sum_partials4<<<1, 256, 0, c->stream>>>(partials, (int)g, sums_dev);
@@ -285,12 +324,30 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   }
   // bind the last variable: final MLE values at (r_0..r_{nv-1})
   Fr vals[MAX_SC_TABLES];
-  for (int i = 0; i < k; i++) {
-    if (nv == 0) {
-      TNS_HIP(hipMemcpyAsync(&vals[i], src[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
-    } else {
-      mle_fold_dev(c, src[i], dst[i], 1, r_prev);
-      TNS_HIP(hipMemcpyAsync(&vals[i], dst[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+  if (tail_rnd < nv) {
+    // src: tables of n >> (tail_rnd - 1) entries; folds by the challenges of rounds
+    // tail_rnd - 1 .. nv - 1 (the last one binds the final variable)
+    const int m = (int)(nv - tail_rnd + 1);
+    tail_ch[m - 1] = r_prev;
+    Fr *d_ch = partials, *d_out = sums_dev;
+    TNS_HIP(hipMemcpyAsync(d_ch, tail_ch, sizeof(Fr) * m, hipMemcpyHostToDevice, c->stream));
+    ScTail tl{};
+    for (int i = 0; i < k; i++) {
+      tl.a[i] = src[i];
+      tl.b[i] = dst[i];
+    }
+    TNS_PROF(c, "sumcheck_round", 96.0 * (double)(n >> (tail_rnd - 1)) * k);
+    k_sc_fold_tail<<<1, 1024, 0, c->stream>>>(tl, k, m, d_ch, d_out);
+    TNS_LAUNCH_CHECK();
+    TNS_HIP(hipMemcpyAsync(vals, d_out, sizeof(Fr) * k, hipMemcpyDeviceToHost, c->stream));
+  } else {
+    for (int i = 0; i < k; i++) {
+      if (nv == 0) {
+        TNS_HIP(hipMemcpyAsync(&vals[i], src[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+      } else {
+        mle_fold_dev(c, src[i], dst[i], 1, r_prev);
+        TNS_HIP(hipMemcpyAsync(&vals[i], dst[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+      }
     }
   }
   TNS_HIP(hipStreamSynchronize(c->stream));
