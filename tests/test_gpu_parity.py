@@ -433,7 +433,9 @@ def _check_twist_properties(pp, addr, val_mont, isw, pr):
     return chals
 
 
-@pytest.mark.parametrize("logn", [10, 14])
+# 10: the whole fold chain runs in k_sc_fold_tail; 13 / 14: one / two k_sc_round folds first
+# (the tail then starts from the scratch / the caller's buffers)
+@pytest.mark.parametrize("logn", [10, 13, 14])
 def test_twist_bench_trace_properties(logn):
     L = logn - 2
     pp, _ = params(L)
@@ -441,10 +443,9 @@ def test_twist_bench_trace_properties(logn):
     pr = ts.Twist(pp).prove_soa(addr, val, isw)
     chals = _check_twist_properties(pp, addr, val, isw, pr)
     # the sum-check fold chain ends at the MLE values at the challenge point
-    if logn <= 10:
-        want = [co.fr_ints(co.mle_evaluate(t, ts.to_mont(chals)))[0]
-                for t in (ts.fr_from_u64_array(addr), val, ts.fr_from_u64_array(isw.astype(np.uint64)))]
-        assert pr.final_mle_evals == want
+    want = [co.fr_ints(co.mle_evaluate(t, ts.to_mont(chals)))[0]
+            for t in (ts.fr_from_u64_array(addr), val, ts.fr_from_u64_array(isw.astype(np.uint64)))]
+    assert pr.final_mle_evals == want
 
 
 def test_twist_ragged_trace_properties():
