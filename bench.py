@@ -4,16 +4,21 @@
 A "step" is one Twist::prove (src/twist.rs:107-252) of the synthetic read/write trace of
 ProtocolBenchmarks (src/benchmarks.rs:88-99) with the trace already resident in HBM:
 C4 = setup_params(22), MemoryTrace::new(2^22), 2^24 operations.  `value` is the
-Twist prover throughput (operations / second, metric as src/benchmarks.rs:26-28), summed
-over ranks.  Multi-GPU runs (torchrun, one process per GPU) prove independent traces per
-rank -- weak scaling, no data-path collective; the timing uses a barrier on both sides
-and the max over ranks.
+Twist prover throughput (operations / second, metric as src/benchmarks.rs:26-28) of the
+whole job.  Multi-GPU runs (torchrun, one process per GPU) by default prove ONE trace of
+N * 2^24 operations sharded over the ranks (the C5 shape): every rank holds a
+2^24-op slice and the ranks exchange per-MSM partial sums, barycentric partials and fold
+values by allgather; value = the operations of that one proof / the max over ranks of the
+timed region (barrier + synchronize on both sides).  --independent instead proves one
+trace per rank with no exchange at all (value = operations summed over ranks / max time).
+Both are weak scaling: 2^24 operations per GPU.
 
 Extra fields (rank 0, N = 1): C2 MSM pairs/s at 2^20 (setup_params(18), Fr::rand scalars
 from ChaCha20Rng([7;32])), C3 Shout lookups/s (2^20-entry table, 2^20 lookups), the per-
 stage device-time breakdown, the roofline of the dominant kernel (HIP events on the
-library's stream; algorithmic bytes from SURVEY.md 8(d)), and the CPU baseline (the C
-oracle restating the reference algorithms, on a bounded sample).
+library's stream; algorithmic bytes from SURVEY.md 8(d)), and two CPU baselines on a
+bounded sample (oracle/fastcpu.c with the GPU path's algorithms, and the C oracle restating
+the reference algorithms).
 """
 
 import argparse

@@ -164,12 +164,15 @@ int tns_msm(tns_ctx *ctx, const tns_srs *srs, const uint64_t *scalars, size_t n,
  * as called by vector_to_polynomial, src/twist.rs:307-315): the n monomial
  * coefficients of the unique interpolant, computed exactly in O(n log^2 n). */
 int tns_interpolate_consecutive(tns_ctx *ctx, const uint64_t *y, size_t n, uint64_t *coeffs);
-/* MultilinearExtension::evaluate (src/polynomials.rs:85-103); variable j <-> index bit j. */
-int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv, const uint64_t *point,
-                     uint64_t out[4]);
+/* MultilinearExtension::evaluate (src/polynomials.rs:85-103); variable j <-> index bit j.
+ * evals holds n_evals <= 2^nv entries (the reference struct's `evaluations`); missing
+ * entries are zero.  n_evals > 2^nv -> TNS_ERR_INVALID_PARAMETERS (the reference's basis
+ * reads only the low nv index bits, so callers fold entry i into i mod 2^nv first). */
+int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, size_t n_evals, unsigned nv,
+                     const uint64_t *point, uint64_t out[4]);
 /* MultilinearExtension::partial_evaluate (src/polynomials.rs:126-161): binds the
- * first k (least-significant) variables; out has 2^(nv-k) entries. */
-int tns_mle_partial_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv,
+ * first k (least-significant) variables; out has 2^(nv-k) entries.  evals as above. */
+int tns_mle_partial_evaluate(tns_ctx *ctx, const uint64_t *evals, size_t n_evals, unsigned nv,
                              const uint64_t *fixed, unsigned k, uint64_t *out);
 
 /* ---------------------------------------------------------------- transcript (src/utils.rs:134-204) */

@@ -433,6 +433,20 @@ int tns_srs_set_tau(tns_srs *srs, const uint64_t tau[4]) {
     if (!srs) throw Error(TNS_ERR_INVALID_PARAMETERS, "null SRS");
     Fr t;
     std::memcpy(&t, tau, 32);
+    // The Lagrange basis (every commitment and opening of the Lagrange route) is derived from
+    // tau, so tau must be the trapdoor of the uploaded powers: one held point g1_powers[e]
+    // (e = 1, or the shard's first index) is checked against tau^e * G1 on the host.  An SRS
+    // holding no such point (only g1_powers[0] = G1) cannot contradict tau.
+    const size_t e = srs->s.first ? srs->s.first : 1;
+    if (e >= srs->s.first && e < srs->s.first + srs->s.held) {
+      TNS_HIP(hipSetDevice(srs->s.device));
+      G1Affine held;
+      TNS_HIP(hipMemcpy(&held, srs->s.points.as<G1Affine>() + (e - srs->s.first), sizeof(G1Affine),
+                        hipMemcpyDeviceToHost));
+      const G1Affine want = xyzz_to_affine(g1_mul_host(g1_generator_host(), pow_u64(t, (u64)e)));
+      if (!(held.x == want.x) || !(held.y == want.y))
+        throw Error(TNS_ERR_INVALID_PARAMETERS, "tau does not match the SRS (g1_powers[e] != tau^e * G1)");
+    }
     for (auto &kv : srs->s.lagrange) delete kv.second;
     srs->s.lagrange.clear();
     srs->s.tau = t;
@@ -609,14 +623,25 @@ int tns_interpolate_consecutive(tns_ctx *ctx, const uint64_t *y, size_t n, uint6
   });
 }
 
-int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv, const uint64_t *point, uint64_t out[4]) {
+// The 2^nv-entry table of an MLE from the caller's n_evals entries: entries past n_evals are
+// zero (the reference's evaluate sums over the entries it holds, src/polynomials.rs:91-102);
+// more than 2^nv entries is rejected (callers fold aliases first).
+static Fr *upload_mle(tns_ctx *ctx, const uint64_t *evals, size_t n_evals, unsigned nv, DevBuf &d) {
+  if (nv > 30) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many variables");
+  const size_t n = (size_t)1 << nv;
+  if (n_evals > n) throw Error(TNS_ERR_INVALID_PARAMETERS, "more evaluations than 2^num_vars");
+  Fr *pe = (Fr *)d.ensure(sizeof(Fr) * n);
+  if (n_evals) TNS_HIP(hipMemcpyAsync(pe, evals, sizeof(Fr) * n_evals, hipMemcpyHostToDevice, ctx->c.stream));
+  if (n_evals < n) TNS_HIP(hipMemsetAsync(pe + n_evals, 0, sizeof(Fr) * (n - n_evals), ctx->c.stream));
+  return pe;
+}
+
+int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, size_t n_evals, unsigned nv, const uint64_t *point,
+                     uint64_t out[4]) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
-    if (nv > 30) throw Error(TNS_ERR_INVALID_PARAMETERS, "too many variables");
-    size_t n = (size_t)1 << nv;
     DevBuf d;
-    Fr *pe = (Fr *)d.ensure(sizeof(Fr) * n);
-    TNS_HIP(hipMemcpyAsync(pe, evals, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
+    Fr *pe = upload_mle(ctx, evals, n_evals, nv, d);
     std::vector<Fr> pt(nv ? nv : 1);
     if (nv) std::memcpy(pt.data(), point, 32 * (size_t)nv);
     Fr r = mle_evaluate_dev(&ctx->c, pe, nv, pt.data());
@@ -625,15 +650,15 @@ int tns_mle_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv, const uin
   });
 }
 
-int tns_mle_partial_evaluate(tns_ctx *ctx, const uint64_t *evals, unsigned nv, const uint64_t *fixed,
-                             unsigned k, uint64_t *out) {
+int tns_mle_partial_evaluate(tns_ctx *ctx, const uint64_t *evals, size_t n_evals, unsigned nv,
+                             const uint64_t *fixed, unsigned k, uint64_t *out) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
     if (k > nv) throw Error(TNS_ERR_INVALID_PARAMETERS, "Cannot fix more variables than available");
-    size_t n = (size_t)1 << nv;
+    const size_t n = (size_t)1 << nv;
     DevBuf a, b;
-    Fr *pa = (Fr *)a.ensure(sizeof(Fr) * n), *pb = (Fr *)b.ensure(sizeof(Fr) * (n / 2 + 1));
-    TNS_HIP(hipMemcpyAsync(pa, evals, sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
+    Fr *pa = upload_mle(ctx, evals, n_evals, nv, a);
+    Fr *pb = (Fr *)b.ensure(sizeof(Fr) * (n / 2 + 1));
     Fr *src = pa, *dst = pb;
     for (unsigned j = 0; j < k; j++) {
       Fr r;

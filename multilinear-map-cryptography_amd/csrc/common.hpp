@@ -402,6 +402,7 @@ void pairing_value(const G1Affine &P, const G2Affine &Q, Fq out[12]);
 
 // verify.cpp: the reference verifiers (host)
 G1Xyzz g1_mul_host(const G1Affine &P, const Fr &k);
+G1Affine g1_generator_host();
 void verifier_key(const Fr &tau, G1Affine *g1, G2Affine *g2, G2Affine *g2_tau);
 bool kzg_verify_host(const G1Affine &g1, const G2Affine &g2, const G2Affine &g2_tau, const G1Affine &C,
                      const Fr &z, const Fr &v, const G1Affine &pi);

@@ -586,14 +586,27 @@ class MultilinearExtension:
         ev[index] = 1
         return cls(num_vars, ev)
 
+    def _table(self) -> np.ndarray:
+        """The evaluations as the device table: at most 2^num_vars entries (the C side
+        zero-fills the rest).  The reference struct may hold any number of entries; its basis
+        reads only the low num_vars index bits (:108-122), so entry i counts at i mod 2^nv."""
+        size = 1 << self.num_vars
+        ev = self.evaluations
+        if len(ev) > size:
+            folded = [0] * size
+            for i, e in enumerate(ev):
+                folded[i & (size - 1)] = (folded[i & (size - 1)] + e) % R_MOD
+            ev = folded
+        return _nonempty(to_mont(ev) if ev else np.zeros((0, 4), dtype=np.uint64))
+
     def evaluate(self, point: Sequence[int], device: int = 0) -> int:  # :85-103
         if len(point) != self.num_vars:
             raise AssertionError("Point dimension must match number of variables")
-        ev = to_mont(self.evaluations)
+        ev = self._table()
         pt = _nonempty(to_mont(list(point)))
         out = np.zeros(4, dtype=np.uint64)
-        _check(N.load().tns_mle_evaluate(Context.get(device).handle, N.p64(ev), self.num_vars, N.p64(pt),
-                                         N.p64(out)))
+        _check(N.load().tns_mle_evaluate(Context.get(device).handle, N.p64(ev), min(len(self.evaluations), 1 << self.num_vars),
+                                         self.num_vars, N.p64(pt), N.p64(out)))
         return from_mont(out)[0]
 
     def partial_evaluate(self, fixed: Sequence[int], device: int = 0) -> "MultilinearExtension":  # :126-161
@@ -602,10 +615,11 @@ class MultilinearExtension:
             raise AssertionError("Cannot fix more variables than available")
         if k == 0:
             return MultilinearExtension(self.num_vars, list(self.evaluations))
-        ev = to_mont(self.evaluations)
+        ev = self._table()
         fx = to_mont(list(fixed))
         out = np.zeros((1 << (self.num_vars - k), 4), dtype=np.uint64)
-        _check(N.load().tns_mle_partial_evaluate(Context.get(device).handle, N.p64(ev), self.num_vars,
+        _check(N.load().tns_mle_partial_evaluate(Context.get(device).handle, N.p64(ev),
+                                                 min(len(self.evaluations), 1 << self.num_vars), self.num_vars,
                                                  N.p64(fx), k, N.p64(out)))
         return MultilinearExtension(self.num_vars - k, from_mont(out))
 
@@ -728,8 +742,26 @@ class TwistProof:
         return TwistProof(u["comms"][0], u["comms"][1], u["sc"], u["openings"], u["finals"])
 
 
-def _pack_proof(commitments, rounds, final_eval, openings, finals) -> N.TnsProof:
-    """Proof fields (affine points / ints) -> the C proof struct (for the verifiers)."""
+def _pack_proof(commitments, rounds, final_eval, openings, finals, verify: bool = False) -> N.TnsProof:
+    """Proof fields (affine points / ints) -> the C proof struct.
+
+    verify=True follows Twist/Shout::verify (src/twist.rs:276, src/shout.rs:245): the openings
+    are checked only when there are at least two opening proofs AND two final evaluations,
+    and then only the first two of each; otherwise they are skipped.  For serialisation the
+    proof must hold exactly 0 or 2 of each (the wire format's Vec lengths).  Round
+    polynomials have the 4 coefficients the prover emits (src/sumcheck.rs:201-206) and there
+    are at most TNS_MAX_ROUNDS of them."""
+    if len(rounds) > N.TNS_MAX_ROUNDS:
+        raise InvalidParameters(f"more than {N.TNS_MAX_ROUNDS} sum-check rounds")
+    for coeffs in rounds:
+        if len(coeffs) != 4:
+            raise InvalidParameters("a round polynomial must have 4 coefficients")
+    if verify:
+        n_open = 2 if min(len(openings), len(finals)) >= 2 else 0
+    else:
+        if len(openings) != len(finals) or len(openings) not in (0, 2):
+            raise InvalidParameters("a proof holds 0 or 2 openings and as many final evaluations")
+        n_open = len(openings)
     pr = N.TnsProof()
     for i, c in enumerate(commitments):
         pr.commitments[i] = (C.c_uint64 * 12)(*_affine_to_proj(c))
@@ -739,11 +771,10 @@ def _pack_proof(commitments, rounds, final_eval, openings, finals) -> N.TnsProof
         for x in range(4):
             pr.round_polynomials[r][x] = (C.c_uint64 * 4)(*m[x])
     pr.final_evaluation = (C.c_uint64 * 4)(*to_mont([final_eval])[0])
-    pr.num_openings = len(openings)
-    for i, o in enumerate(openings):
-        pr.opening_proofs[i] = (C.c_uint64 * 12)(*_affine_to_proj(o))
-    for i, v in enumerate(finals):
-        pr.final_evaluations[i] = (C.c_uint64 * 4)(*to_mont([v])[0])
+    pr.num_openings = n_open
+    for i in range(n_open):
+        pr.opening_proofs[i] = (C.c_uint64 * 12)(*_affine_to_proj(openings[i]))
+        pr.final_evaluations[i] = (C.c_uint64 * 4)(*to_mont([finals[i]])[0])
     return pr
 
 
@@ -809,7 +840,7 @@ class Twist:
         """src/twist.rs:255-304 (host: sum-check replay + two pairing checks)."""
         pr = _pack_proof([proof.address_commitment.commitment, proof.value_commitment.commitment],
                          proof.consistency_proof.round_polynomials, proof.consistency_proof.final_evaluation,
-                         [p.proof for p in proof.opening_proofs], proof.final_evaluations)
+                         [p.proof for p in proof.opening_proofs], proof.final_evaluations, verify=True)
         ok = C.c_int()
         _check(N.load().tns_twist_verify(C.byref(verifier_params.commitment_vk.raw), C.byref(pr), C.byref(ok)))
         return bool(ok.value)
@@ -909,7 +940,7 @@ class Shout:
         """src/shout.rs:225-274"""
         pr = _pack_proof([proof.table_commitment.commitment, proof.index_commitment.commitment],
                          proof.lookup_proof.round_polynomials, proof.lookup_proof.final_evaluation,
-                         [p.proof for p in proof.opening_proofs], proof.final_evaluations)
+                         [p.proof for p in proof.opening_proofs], proof.final_evaluations, verify=True)
         ok = C.c_int()
         _check(N.load().tns_shout_verify(C.byref(verifier_params.commitment_vk.raw), C.byref(pr), C.byref(ok)))
         return bool(ok.value)

@@ -92,8 +92,8 @@ SIGNATURES = [
     ("tns_commitment_hash", C.c_int, [U64P, U64P]),
     ("tns_msm", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_interpolate_consecutive", C.c_int, [C.c_void_p, U64P, C.c_size_t, U64P]),
-    ("tns_mle_evaluate", C.c_int, [C.c_void_p, U64P, C.c_uint, U64P, U64P]),
-    ("tns_mle_partial_evaluate", C.c_int, [C.c_void_p, U64P, C.c_uint, U64P, C.c_uint, U64P]),
+    ("tns_mle_evaluate", C.c_int, [C.c_void_p, U64P, C.c_size_t, C.c_uint, U64P, U64P]),
+    ("tns_mle_partial_evaluate", C.c_int, [C.c_void_p, U64P, C.c_size_t, C.c_uint, U64P, C.c_uint, U64P]),
     ("tns_transcript_new", C.c_void_p, [U8P]),
     ("tns_transcript_free", None, [C.c_void_p]),
     ("tns_transcript_append_field_element", None, [C.c_void_p, U8P, C.c_size_t, U64P]),

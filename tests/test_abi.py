@@ -122,3 +122,13 @@ def test_memory_trace_and_lookup_table_bookkeeping():
     assert a.sum_evaluations() == 3
     with pytest.raises(AssertionError):
         ts.MultilinearExtension.from_evaluations([1] * 7)
+
+
+def test_mle_table_follows_reference_struct():
+    # MultilinearExtension's fields are public (src/polynomials.rs:18-24): evaluate sums over
+    # the entries the struct holds, each at its low num_vars index bits (:91-122)
+    m = ts.MultilinearExtension(2, [1, 2])  # short: missing entries are zero
+    assert ts.from_mont(m._table()) == [1, 2]
+    m = ts.MultilinearExtension(1, [1, 2, 3, 4, 5])  # long: entry i counts at i mod 2
+    assert ts.from_mont(m._table()) == [1 + 3 + 5, 2 + 4]
+    assert ts.from_mont(ts.MultilinearExtension(0, [])._table()) == [0]

@@ -164,6 +164,21 @@ def test_uploaded_srs_with_small_tau_uses_coefficients_on_nodes():
         assert pi.proof == po.affine_mul(po.G1_GEN, q_tau)
 
 
+def test_uploaded_srs_rejects_mismatched_tau():
+    # the Lagrange basis is derived from tau: a tau that is not the powers' trapdoor would
+    # give silently wrong commitments, so set_tau checks g1_powers[1] == tau * G1
+    with pytest.raises(ts.InvalidParameters):
+        ts.CommitmentParams.from_g1_powers(_srs_from_tau(5, 8), tau=6)
+    pp, _ = params(3)
+    with pytest.raises(ts.InvalidParameters):
+        ts.CommitmentParams.from_g1_powers(pp.commitment_params.g1_powers, tau=pp.commitment_params.tau + 1)
+    cp = ts.CommitmentParams.from_g1_powers(pp.commitment_params.g1_powers, tau=pp.commitment_params.tau)
+    ys = rand_vals(8, seed=3)
+    assert ts.KZGCommitment.commit_evaluations(cp, ys).commitment == oracle_commit_evals(3, ys)
+    # a one-point SRS (g1_powers[0] = G1 only) cannot contradict tau
+    ts.CommitmentParams.from_g1_powers(_srs_from_tau(5, 1), tau=6)
+
+
 def test_uploaded_srs_without_tau_matches_setup_srs():
     pp, _ = params(3)
     pts = pp.commitment_params.g1_powers

@@ -245,6 +245,25 @@ def test_mle_reference_kats():
     assert s.evaluate([0, 0, 0]) == 100 and s.evaluate([1, 1, 1]) == 700 and s.evaluate([1, 1, 0]) == 0
 
 
+def test_mle_struct_with_any_entry_count():
+    # the struct's fields are public (src/polynomials.rs:18-24): evaluate sums over the entries
+    # held, each at its low num_vars index bits (:91-122) -- short and long vectors included
+    pt = [5, 7, 11]
+    short = ts.MultilinearExtension(3, [1, 2])
+    assert short.evaluate(pt) == po.mle_evaluate([1, 2] + [0] * 6, pt)
+    long_ = ts.MultilinearExtension(2, list(range(1, 11)))
+    folded = [sum(v for i, v in enumerate(range(1, 11)) if i % 4 == j) % R for j in range(4)]
+    assert long_.evaluate(pt[:2]) == po.mle_evaluate(folded, pt[:2])
+    assert short.partial_evaluate([3]).evaluations == ts.MultilinearExtension(3, [1, 2] + [0] * 6).partial_evaluate(
+        [3]).evaluations
+    assert ts.MultilinearExtension(2, []).evaluate([1, 2]) == 0
+    import twist_and_shout._native as N
+    ev = ts.to_mont([1, 2, 3, 4, 5])
+    out = np.zeros(4, dtype=np.uint64)
+    st = N.load().tns_mle_evaluate(ts.Context.get(0).handle, N.p64(ev), 5, 2, N.p64(ts.to_mont([1, 2])), N.p64(out))
+    assert st == 1  # more entries than 2^nv: InvalidParameters at the C ABI
+
+
 @pytest.mark.parametrize("nv", [0, 1, 2, 5, 10, 14])
 def test_mle_evaluate_matches_oracle(nv):
     ev = rand_fr_mont(1 << nv, seed=nv)
@@ -252,7 +271,7 @@ def test_mle_evaluate_matches_oracle(nv):
     import twist_and_shout._native as N
     import ctypes as C
     out = np.zeros(4, dtype=np.uint64)
-    st = N.load().tns_mle_evaluate(ts.Context.get(0).handle, N.p64(ev), nv,
+    st = N.load().tns_mle_evaluate(ts.Context.get(0).handle, N.p64(ev), len(ev), nv,
                                    N.p64(np.ascontiguousarray(pt) if nv else np.zeros((1, 4), dtype=np.uint64)),
                                    N.p64(out))
     assert st == 0

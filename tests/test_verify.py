@@ -146,3 +146,45 @@ def test_protocol_verify_matches_oracle(golden, vk):
             [[h(c) for c in r] for r in case["round_polynomials"]], h(case["final_evaluation"]),
             [g1h(p) for p in case["opening_proofs"]], [h(v) for v in case["final_evaluations"]])
     assert po.protocol_verify(ovk, bytes(32), (b"address_commitment", b"value_commitment"), *args)
+
+
+def test_verify_opening_counts_follow_reference(golden, vk):
+    # src/twist.rs:276: the openings are checked only with >= 2 opening proofs AND >= 2 final
+    # evaluations, and then only the first two of each
+    case = golden["twist"]["demo_L3"]
+    few = _twist_proof(case)
+    few.final_evaluations = few.final_evaluations[:1]
+    few.final_evaluations[0] = (few.final_evaluations[0] + 1) % R  # would fail if it were checked
+    assert ts.Twist.verify(few, _vp(vk))
+    none = _twist_proof(case)
+    none.opening_proofs = []
+    assert ts.Twist.verify(none, _vp(vk))
+    extra = _twist_proof(case)
+    extra.opening_proofs.append(ts.KZGProof(po.affine_mul(po.G1_GEN, 9)))
+    extra.final_evaluations.append(123)
+    assert ts.Twist.verify(extra, _vp(vk))  # extras are ignored
+    extra.final_evaluations[1] = (extra.final_evaluations[1] + 1) % R
+    assert not ts.Twist.verify(extra, _vp(vk))
+    sh = golden["shout"]
+    name = next(iter(sh))
+    sfew = _shout_proof(sh[name])
+    sfew.opening_proofs = sfew.opening_proofs[:1]
+    assert ts.Shout.verify(sfew, _vp(vk))
+
+
+def test_malformed_proofs_raise(golden, vk):
+    case = golden["twist"]["demo_L3"]
+    bad = _twist_proof(case)
+    bad.consistency_proof.round_polynomials[0] = [0, 0, 0]
+    with pytest.raises(ts.InvalidParameters):
+        ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.consistency_proof.round_polynomials = [[0, 0, 0, 0]] * 41
+    with pytest.raises(ts.InvalidParameters):
+        ts.Twist.verify(bad, _vp(vk))
+    bad = _twist_proof(case)
+    bad.opening_proofs = bad.opening_proofs[:1]
+    with pytest.raises(ts.InvalidParameters):  # the wire format holds 0 or 2 openings
+        bad.serialize()
+    good = _twist_proof(case)
+    assert ts.TwistProof.deserialize(good.serialize()).opening_proofs == good.opening_proofs
