@@ -427,7 +427,8 @@ __device__ __forceinline__ G1Xyzz xyzz_madd_lazy(const G1Xyzz &p, const G1Affine
   const Fq Q = mul_lazy_dev(p.x, PP);
   G1Xyzz r;
   r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
-  r.y = sub2_dev(mul_lazy_dev(R, sub2_dev(Q, r.x)), mul_lazy_dev(p.y, PPP));
+  // Y3 = R (Q - X3) - Y1 PPP as ONE reduction of R (Q - X3) + Y1 (2M - PPP)
+  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), p.y, sub2_dev(Fq::zero(), PPP));
   r.zz = mul_lazy_dev(p.zz, PP);
   r.zzz = mul_lazy_dev(p.zzz, PPP);
   return r;
@@ -462,7 +463,7 @@ __device__ __forceinline__ G1Xyzz xyzz_add_lazy(const G1Xyzz &p, const G1Xyzz &q
   const Fq Q = mul_lazy_dev(U1, PP);
   G1Xyzz r;
   r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
-  r.y = sub2_dev(mul_lazy_dev(R, sub2_dev(Q, r.x)), mul_lazy_dev(S1, PPP));
+  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), S1, sub2_dev(Fq::zero(), PPP));  // one reduction
   r.zz = mul_lazy_dev(mul_lazy_dev(p.zz, q.zz), PP);
   r.zzz = mul_lazy_dev(mul_lazy_dev(p.zzz, q.zzz), PPP);
   return r;

@@ -194,6 +194,9 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
     const size_t b = a + acc_k < valid ? a + acc_k : valid;
     uint32_t cur = keys[a] >> ks;
     G1Xyzz acc = G1Xyzz::inf();
+    // the gather of entry p + 1 is in flight while entry p is added (the sign is applied at use)
+    uint32_t v_nxt = vals[a];
+    G1Affine q_nxt = pts[v_nxt & 0x7fffffffu];
     for (size_t p = a;; p++) {
       const uint32_t k = (p < b) ? keys[p] >> ks : 0xffffffffu;
       if (k != cur) {  // flush the run of bucket `cur`
@@ -206,7 +209,16 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
         cur = k;
         acc = G1Xyzz::inf();
       }
-      acc = xyzz_madd_lazy(acc, load_signed_point(pts, vals[p]));
+      const uint32_t v = v_nxt;
+      G1Affine q = q_nxt;
+      if (p + 1 < b) {
+        v_nxt = vals[p + 1];
+        q_nxt = pts[v_nxt & 0x7fffffffu];
+      }
+      const Fq ny = sub_dev(Fq::zero(), q.y);  // -y (0 stays 0: the identity is (0, 0))
+#pragma unroll
+      for (int l = 0; l < 8; l++) q.y.v[l] = (v >> 31) ? ny.v[l] : q.y.v[l];
+      acc = xyzz_madd_lazy(acc, q);
     }
   }
 }
