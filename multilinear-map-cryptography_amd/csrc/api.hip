@@ -242,15 +242,17 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
       S[k] = add(S[k], all[4 * (size_t)r + 2 * k + 1]);
     }
   for (int k = 0; k < 2; k++) value[k] = mul(ell[k], S[k]);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
+  // the shared-inverse pass hands the MSMs canonical quotients and their bit lengths
+  unsigned *qbits = same_nodes && p0.cnt > 64 ? (unsigned *)c->qbits.ensure(2 * sizeof(unsigned)) : nullptr;
   if (same_nodes) {
-    lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1);
+    lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1, qbits);
   } else {
     lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
     lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
   }
   G1Xyzz pp[2];
-  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb},
-               MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb}, pp);
+  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits},
+               MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr}, pp);
   allgather_sum_g1_pair(c, m, pp, proof);
 }
 

@@ -178,6 +178,129 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift
   write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, keys, vals);
 }
 
+// ---- pass 1 with a compile-time window plan (C bits, W windows): the digit of window w sits
+// at a constant bit offset, so it is one funnel shift of two known limbs (the runtime plan
+// needs 16 selects per window to avoid a dynamic register index), and each thread keeps its
+// entries' keys and LDS ranks in registers: ONE digit sweep and ONE returning LDS atomic per
+// entry (the runtime kernels sweep twice and count twice).  Each thread owns up to SPT
+// scalars of the tile (tile = spb <= 256 SPT scalars, spb W <= TILE entries).
+template <int C, int W>
+__device__ __forceinline__ uint32_t digit_raw(const Fr &k, int w) {
+  const int bit = w * C, limb = bit >> 5, sh = bit & 31;
+  const uint32_t lo = limb < 8 ? k.v[limb] : 0u, hi = limb + 1 < 8 ? k.v[limb + 1] : 0u;
+  const uint32_t x = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> sh) : lo;
+  return x & ((1u << C) - 1);
+}
+
+// signed digits of one scalar: g(w, key, neg) for every non-zero digit (keys as scalar_digits)
+template <int C, int W, class G>
+__device__ __forceinline__ void scalar_digits_ct(const Fr &k, const DigitArgs &A, G g) {
+  constexpr uint32_t half = 1u << (C - 1);
+  uint32_t carry = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    const uint32_t val = digit_raw<C, W>(k, w) + carry;
+    const bool negd = val > half;
+    const uint32_t mag = negd ? (1u << C) - val : val;
+    carry = negd ? 1u : 0u;
+    if (mag) {
+      const uint32_t key = A.shared ? ((mag - 1) << A.wb) | (uint32_t)w : ((uint32_t)w << (C - 1)) | (mag - 1);
+      g(w, key, negd);
+    }
+  }
+}
+
+template <int C, int W>
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shift, int nbins, size_t T1,
+                                                           uint32_t *__restrict__ counts) {
+  __shared__ uint32_t h[BS_MAXBINS];
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h[d] = 0;
+  __syncthreads();
+  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  for (size_t i0 = a + threadIdx.x; i0 < b; i0 += (size_t)BS_SCALARS * BS_BLOCK) {
+    Fr s[BS_SCALARS];  // the loads in flight together, then the digits
+#pragma unroll
+    for (int j = 0; j < BS_SCALARS; j++)
+      if (i0 + (size_t)j * BS_BLOCK < b) s[j] = A.scalars[i0 + (size_t)j * BS_BLOCK];
+#pragma unroll
+    for (int j = 0; j < BS_SCALARS; j++)
+      if (i0 + (size_t)j * BS_BLOCK < b)
+        scalar_digits_ct<C, W>(s[j], A, [&](int, uint32_t key, bool) { atomicAdd(&h[key >> shift], 1u); });
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) counts[(size_t)d * T1 + tile] = h[d];
+  if (tile == 0 && threadIdx.x == 0) counts[(size_t)nbins * T1] = 0;
+}
+
+constexpr uint32_t BS_NOKEY = 0x40000000u;  // empty entry slot (keys are < 2^30; bit 31 = sign)
+
+template <int TILE, int C, int W, int SPT>
+__global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int shift, int nbins, size_t T1,
+                                                             const uint32_t *__restrict__ offs,
+                                                             uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+  __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
+  __shared__ uint32_t lk[TILE], lv[TILE];
+  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
+    h[d] = 0;
+    goff[d] = offs[(size_t)d * T1 + tile];
+  }
+  __syncthreads();
+  uint32_t ek[SPT][W], er[SPT][W];  // key | sign << 31 (BS_NOKEY: none), rank inside its bin
+  constexpr int LA = SPT < BS_SCALARS ? SPT : BS_SCALARS;  // scalar loads in flight together
+  Fr s[LA];
+#pragma unroll
+  for (int j = 0; j < SPT; j++) {
+    if (j % LA == 0) {
+#pragma unroll
+      for (int q = 0; q < LA; q++) {
+        const size_t iq = a + threadIdx.x + (size_t)(j + q) * BS_BLOCK;
+        if (j + q < SPT && iq < b) s[q] = A.scalars[iq];
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; w++) ek[j][w] = BS_NOKEY;
+    const size_t i = a + threadIdx.x + (size_t)j * BS_BLOCK;
+    if (i < b)
+      scalar_digits_ct<C, W>(s[j % LA], A, [&](int w, uint32_t key, bool negd) {
+        er[j][w] = atomicAdd(&h[key >> shift], 1u);
+        ek[j][w] = key | (negd ? 0x80000000u : 0u);
+      });
+  }
+  __syncthreads();
+  block_scan_bins(h, lbase, nbins, wsum);
+  const int m = (int)(lbase[nbins - 1] + h[nbins - 1]);
+#pragma unroll
+  for (int j = 0; j < SPT; j++) {
+    const size_t i = a + threadIdx.x + (size_t)j * BS_BLOCK;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint32_t e = ek[j][w];
+      if (e != BS_NOKEY) {
+        const uint32_t key = e & 0x7fffffffu;
+        const uint32_t slot = lbase[key >> shift] + er[j][w];
+        lk[slot] = key;
+        lv[slot] = (uint32_t)(A.shared ? (size_t)w * A.stride + i : i) | (e & 0x80000000u);
+      }
+    }
+  }
+  __syncthreads();
+  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, keys, vals);
+}
+
+// compile-time plans of the pass-1 kernels: the fixed-base table windows (n = 2^20..2^26) and
+// the narrow trace commitments' per-window plans; anything else takes the runtime kernels
+struct Pass1Plan {
+  int c, W;
+  void (*count)(DigitArgs, int, int, size_t, uint32_t *);
+  void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, uint32_t *, uint32_t *);
+  int spt;
+};
+#define TNS_P1(C, W, SPT) {C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<BS_TILE, C, W, SPT>, SPT}
+static const Pass1Plan kPass1Plans[] = {TNS_P1(22, 12, 3), TNS_P1(20, 13, 3), TNS_P1(19, 14, 3), TNS_P1(17, 15, 3),
+                                        TNS_P1(16, 2, 16), TNS_P1(12, 2, 16)};
+#undef TNS_P1
+
 // bins of pass 1 -> segment starts; seg[nbins] = total = number of entries (also *valid)
 __global__ void k_bs_segs1(const uint32_t *__restrict__ offs, int nbins, size_t T1, uint32_t *__restrict__ seg,
                            uint32_t *__restrict__ valid) {
@@ -186,9 +309,14 @@ __global__ void k_bs_segs1(const uint32_t *__restrict__ offs, int nbins, size_t 
 }
 
 // tiles per segment
-__global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t tile, uint32_t *__restrict__ tcount) {
-  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s <= S; s += (size_t)gridDim.x * blockDim.x)
-    tcount[s] = s < S ? (uint32_t)((seg[s + 1] - seg[s] + tile - 1) / tile) : 0u;
+// tiles per segment; mcount (optional): the same for segments of >= 2 tiles, else 0
+__global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t tile, uint32_t *__restrict__ tcount,
+                           uint32_t *__restrict__ mcount) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s <= S; s += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t t = s < S ? (uint32_t)((seg[s + 1] - seg[s] + tile - 1) / tile) : 0u;
+    tcount[s] = t;
+    if (mcount) mcount[s] = t > 1 ? t : 0u;
+  }
 }
 
 // desc[tile_base[s] + k] = s for the tiles k of segment s
@@ -201,7 +329,28 @@ struct PassGeom {
   const uint32_t *seg, *tbase, *desc;
   int shift, nbins;
   uint32_t mask;
+  int ident;              // every segment is one tile: tile g = segment g (tbase / desc unused)
+  const uint32_t *mbase;  // set: the counts hold only segments of >= 2 tiles, segment s's block at
+                          // nbins * mbase[s] (exclusive scan of their tile counts); else at nbins * tbase[s]
 };
+
+// the first count slot of segment s (its first tile tb)
+__device__ __forceinline__ size_t count_base(const PassGeom &G, uint32_t s, uint32_t tb) {
+  return (size_t)G.nbins * (G.mbase ? G.mbase[s] : tb);
+}
+
+// tile g's segment s, the segment's first tile tb and its tile count Ts
+__device__ __forceinline__ void tile_geom(const PassGeom &G, size_t g, uint32_t &s, uint32_t &tb, uint32_t &Ts) {
+  if (G.ident) {
+    s = tb = (uint32_t)g;
+    Ts = 1;
+  } else {
+    s = G.desc[g];
+    tb = G.tbase[s];
+    Ts = G.tbase[s + 1] - tb;
+  }
+}
+
 
 // passes >= 2, histogram: counts[nbins * tbase[s] + d * T_s + k]
 template <int TILE>
@@ -209,17 +358,21 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
                                                        const uint32_t *__restrict__ keys, uint32_t *__restrict__ counts) {
   __shared__ uint32_t h[BS_MAXBINS];
   const size_t g = blockIdx.x;
-  if (g == max_tiles - 1 && threadIdx.x == 0) counts[(size_t)G.nbins * max_tiles] = 0;
-  if (g >= G.tbase[S]) {  // unused tile slot: zero its share of the scan input
-    for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * g + d] = 0;
-    return;
+  if (!G.mbase) {  // full layout over max_tiles slots (the compact one is sized exactly by the host)
+    if (g == max_tiles - 1 && threadIdx.x == 0) counts[(size_t)G.nbins * max_tiles] = 0;
+    if (g >= G.tbase[S]) {  // unused tile slot: zero its share of the scan input
+      for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * g + d] = 0;
+      return;
+    }
   }
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) h[d] = 0;
   __syncthreads();
-  const uint32_t s = G.desc[g];
-  const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  uint32_t s, tb, Ts;
+  tile_geom(G, g, s, tb, Ts);
+  const uint32_t k = (uint32_t)g - tb;
   if (Ts == 1) {  // a one-tile segment: k_bs_scatter ranks it locally (no keys read here)
-    for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + d] = 0;
+    if (!G.mbase)
+      for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + d] = 0;
     return;
   }
   constexpr int IPT = TILE / BS_BLOCK;
@@ -234,7 +387,8 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
   for (int j = 0; j < IPT; j++)
     if (a + threadIdx.x + (size_t)j * BS_BLOCK < e) atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
   __syncthreads();
-  for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[(size_t)G.nbins * tb + (size_t)d * Ts + k] = h[d];
+  const size_t cb = count_base(G, s, tb);
+  for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[cb + (size_t)d * Ts + k] = h[d];
 }
 
 // passes >= 2, scatter: tile -> LDS ordered by bin -> coalesced runs.  Segment s's block of
@@ -251,14 +405,16 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
   constexpr int IPT = TILE / BS_BLOCK;
   __shared__ uint32_t lk[TILE], lv[TILE];
   const size_t g = blockIdx.x;
-  if (g >= G.tbase[S]) return;
-  const uint32_t s = G.desc[g];
-  const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb, k = (uint32_t)g - tb;
+  if (g >= (G.ident ? S : G.tbase[S])) return;
+  uint32_t s, tb, Ts;
+  tile_geom(G, g, s, tb, Ts);
+  const uint32_t k = (uint32_t)g - tb;
   const uint32_t s0 = G.seg[s];
-  const uint32_t base = Ts == 1 ? 0u : s0 - offs[(size_t)G.nbins * tb];
+  const size_t cb = Ts == 1 ? 0 : count_base(G, s, tb);
+  const uint32_t base = Ts == 1 ? 0u : s0 - offs[cb];
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) {
     h[d] = 0;
-    if (Ts != 1) goff[d] = base + offs[(size_t)G.nbins * tb + (size_t)d * Ts + k];
+    if (Ts != 1) goff[d] = base + offs[cb + (size_t)d * Ts + k];
   }
   const size_t a = s0 + (size_t)k * TILE, e = min((size_t)G.seg[s + 1], a + TILE);
   const int m = (int)(e - a);
@@ -303,10 +459,12 @@ __global__ void k_bs_segs(PassGeom G, size_t S, const uint32_t *__restrict__ off
       nseg[NS] = G.seg[S];
       continue;
     }
+    if (G.ident) continue;  // every segment was ranked locally (k_bs_scatter wrote nseg)
     const size_t s = id / G.nbins, d = id % G.nbins;
     const uint32_t tb = G.tbase[s], Ts = G.tbase[s + 1] - tb;
     if (Ts == 1) continue;
-    nseg[id] = Ts ? G.seg[s] + (offs[(size_t)G.nbins * tb + d * Ts] - offs[(size_t)G.nbins * tb]) : G.seg[s];
+    const size_t cb = count_base(G, (uint32_t)s, tb);
+    nseg[id] = Ts ? G.seg[s] + (offs[cb + d * Ts] - offs[cb]) : G.seg[s];
   }
 }
 
@@ -326,13 +484,14 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const T *in, T *out, siz
 
 // tile size of pass p (0-based; 8192 or 4096 entries).  TNS_BS_TILES="t0,t1,t2" overrides
 // (tuning); passes beyond the list use its last entry.
+// 0 = automatic: 8192, except a last pass whose segments average <= 3584 entries (4096: the
+// one-tile segments fill it, and half the LDS doubles the blocks per CU -- pass 3 of a 2^24
+// opening MSM 1.02 -> 0.61 ms, profiles/r02_ab_sort_tiles.txt).
 static int pass_tile(int p) {
   static int t[8] = {0};
   static int nt = 0;
   if (!nt) {
-    int def[3] = {8192, 8192, 8192};
-    for (int i = 0; i < 3; i++) t[i] = def[i];
-    nt = 3;
+    nt = 1;  // t[0] = 0: automatic
     if (const char *e = getenv("TNS_BS_TILES")) {
       int k = 0;
       for (const char *q = e; *q && k < 8;) {
@@ -366,13 +525,37 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   const int keybits = bucket_bits + A.wb;
   const int npass = std::max(1, (keybits + BS_MAXBITS - 1) / BS_MAXBITS);
   int bits[8] = {0};
-  bits[0] = keybits - BS_MAXBITS * (npass - 1);  // the smallest split first: pass-1 runs stay long
-  for (int p = 1; p < npass; p++) bits[p] = BS_MAXBITS;
+  // the last pass sorts LDS-sized segments by BS_MAXBITS bits; the passes before it split the
+  // remaining bits evenly (25-bit keys: 8, 8, 9 -- pass 2 with 256 instead of 512 bins writes
+  // 128-byte runs: 1.21 -> 1.02 ms at 2^24)
+  bits[npass - 1] = std::min(keybits, BS_MAXBITS);
+  for (int p = 0, rest = keybits - bits[npass - 1]; p < npass - 1; p++) {
+    bits[p] = (rest + (npass - 2 - p)) / (npass - 1 - p);
+    rest -= bits[p];
+  }
+  if (const char *e = getenv("TNS_BS_BITS")) {  // tuning: "b0,b1,..." (each <= 9, summing to keybits)
+    int v[8], k = 0, sum = 0;
+    for (const char *q = e; *q && k < 8;) {
+      v[k] = atoi(q);
+      sum += v[k++];
+      while (*q && *q != ',') q++;
+      if (*q == ',') q++;
+    }
+    bool ok = k == npass && sum == keybits;
+    for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= BS_MAXBITS;
+    if (ok)
+      for (int p = 0; p < npass; p++) bits[p] = v[p];
+  }
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
-  const int tile1 = W <= 4096 ? pass_tile(0) : BS_TILE;
+  const int tile1 = W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
+  const Pass1Plan *ct = nullptr;
+  if (tile1 == BS_TILE && !getenv("TNS_BS_RUNTIME_PASS1"))  // (A/B: the runtime-plan kernels)
+    for (const Pass1Plan &p : kPass1Plans)
+      if (p.c == c && p.W == W) ct = &p;
   A.spb = (size_t)tile1 / W;
+  if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
   const size_t T1 = (n + A.spb - 1) / A.spb;
   int nb = 1 << bits[0];
   const size_t max_seg = (size_t)1 << keybits;
@@ -382,10 +565,12 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
   uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
-  k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+  if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+  else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
   TNS_LAUNCH_CHECK();
   exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
-  if (tile1 == 4096) k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  if (ct) ct->scatter<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  else if (tile1 == 4096) k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
   else k_bs_scatter1<BS_TILE><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
   TNS_LAUNCH_CHECK();
   k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
@@ -399,18 +584,44 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   for (int p = 1; p < npass; p++) {
     nb = 1 << bits[p];
     shift -= bits[p];
-    const int tile = pass_tile(p);
-    const size_t tiles_bound = (E + tile - 1) / tile + S;
-    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, (uint32_t)tile, tcount);
+    int tile = pass_tile(p);
+    if (!tile) tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
+    // In the last pass most segments fit one tile and rank locally; only segments of >= 2
+    // tiles need the histogram pass and the global scan, so their counts get a compact layout,
+    // sized from a readback of the tile totals (the top window's narrow digits make the
+    // low-magnitude buckets' segments multi-tile).  All one-tile: no geometry at all (at 2^24
+    // the full layout's histograms and scan over 512 bins x every tile took 0.34 ms).
+    int ident = 0;
+    const uint32_t *mb = nullptr;
+    size_t tiles_bound = (E + tile - 1) / tile + S, scan_len = (size_t)nb * tiles_bound + 1;
+    uint32_t *mcount = (uint32_t *)ln.ws[17].ensure(sizeof(uint32_t) * 2 * (max_seg + 1)), *mbase = mcount + (max_seg + 1);
+    const bool last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
+    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, (uint32_t)tile, tcount, last ? mcount : nullptr);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], tcount, tbase, S + 1);
-    k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(tbase, S, desc);
-    TNS_LAUNCH_CHECK();
-    PassGeom G{seg[cur], tbase, desc, shift, nb, (uint32_t)nb - 1};
-    if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
-    else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
-    TNS_LAUNCH_CHECK();
-    exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * tiles_bound + 1);
+    if (last) {
+      exclusive_scan(st, ln.ws[9], mcount, mbase, S + 1);
+      uint32_t *h = (uint32_t *)ln.host2.ensure(2 * sizeof(uint32_t));
+      TNS_HIP(hipMemcpyAsync(h, tbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      TNS_HIP(hipMemcpyAsync(h + 1, mbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      TNS_HIP(hipStreamSynchronize(st));
+      ident = h[1] == 0;
+      tiles_bound = ident ? S : h[0];
+      mb = mbase;
+      scan_len = (size_t)nb * h[1] + 1;
+    }
+    if (!ident) {
+      k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(tbase, S, desc);
+      TNS_LAUNCH_CHECK();
+    }
+    PassGeom G{seg[cur], tbase, desc, shift, nb, (uint32_t)nb - 1, ident, mb};
+    if (!ident) {
+      if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
+      if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
+      else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
+      TNS_LAUNCH_CHECK();
+      exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
+    }
     if (tile == 4096)
       k_bs_scatter<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1],
                                                                      V[cur ^ 1], seg[cur ^ 1]);

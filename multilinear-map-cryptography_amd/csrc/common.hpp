@@ -97,9 +97,10 @@ struct PinnedBuf {
 // (the two commitments, the two opening quotients) overlap on the device.
 struct MsmLane {
   hipStream_t stream = nullptr;
-  DevBuf ws[17];
+  DevBuf ws[18];
   DevBuf fix;       // heavy-bucket level sums
   PinnedBuf host;   // scalar bit length, then the per-set sums
+  PinnedBuf host2;  // bucket sort: the largest last-pass segment
 };
 
 // Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).
@@ -238,6 +239,7 @@ struct Ctx {
   std::mutex mu;
   // workspaces
   DevBuf scratch[8];
+  DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
   DevBuf twiddles;  // omega_{2^k}^i, i < 2^(k-1), natural order, for the largest k seen
@@ -328,11 +330,22 @@ void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
 G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr);
+// bit length of a canonical field element (0 for zero)
+__device__ __forceinline__ unsigned fr_bit_length(const Fr &k) {
+  unsigned b = 0;
+#pragma unroll
+  for (int l = 0; l < 8; l++)
+    if (k.v[l]) b = 32 * l + 32 - __builtin_clz(k.v[l]);
+  return b;
+}
 struct MsmArgs {
   const G1Affine *points;
   const Fr *scalars;
   size_t n;
   const FixedBase *fb;
+  // set: `scalars` are CANONICAL (not Montgomery) and their largest bit length is at this
+  // device address (n > 64 only: the tiny path reads Montgomery scalars)
+  const unsigned *canon_bits = nullptr;
 };
 // two independent MSMs overlapped on the context's two lanes (inputs ready on c->stream)
 void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
@@ -367,8 +380,9 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
 void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
                                 Fr *inv, Fr parts[3]);
+// bits != nullptr: q0 / q1 come out CANONICAL with their largest bit lengths in bits[0..1]
 void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
-                                   const Fr *inv, Fr *q0, Fr *q1);
+                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits);
 // quotient values for an opening AT the node j0 (value y_j0), unsharded
 void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q);
 bool fr_is_node(const Fr &x, size_t N);

@@ -157,6 +157,31 @@ __global__ void __launch_bounds__(256) k_node_quotient2(const Fr *__restrict__ y
   }
 }
 
+// k_node_quotient2 producing what the two opening MSMs consume: the CANONICAL quotient values
+// (the bucket sort reads digits of canonical scalars) and each vector's largest bit length
+// (the MSM's window plan) -- msm.hip's k_scalar_bits pass over q0 / q1 is folded in here.
+__global__ void __launch_bounds__(256) k_node_quotient2_canon(const Fr *__restrict__ y0, const Fr *__restrict__ y1,
+                                                              Fr v0, Fr v1, size_t n, const Fr *invs,
+                                                              Fr *__restrict__ q0, Fr *q1, unsigned *__restrict__ bits) {
+  unsigned b0 = 0, b1 = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const Fr iv = invs[i];
+    const Fr c0 = from_mont(mul(sub(v0, y0[i]), iv)), c1 = from_mont(mul(sub(v1, y1[i]), iv));
+    q0[i] = c0;
+    q1[i] = c1;
+    b0 = max(b0, fr_bit_length(c0));
+    b1 = max(b1, fr_bit_length(c1));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    b0 = max(b0, (unsigned)__shfl_xor(b0, o));
+    b1 = max(b1, (unsigned)__shfl_xor(b1, o));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (b0) atomicMax(bits, b0);
+    if (b1) atomicMax(bits + 1, b1);
+  }
+}
+
 // q_i = (v - y_i) * inv_i, in place over inv
 __global__ void __launch_bounds__(256) k_node_quotient(const Fr *__restrict__ y, Fr v, size_t n, Fr *__restrict__ q) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -352,9 +377,14 @@ void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, si
 }
 
 void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
-                                   const Fr *inv, Fr *q0, Fr *q1) {
+                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits) {
   TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);
-  k_node_quotient2<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1);
+  if (bits) {
+    TNS_HIP(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned), c->stream));
+    k_node_quotient2_canon<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1, bits);
+  } else {
+    k_node_quotient2<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1);
+  }
   TNS_LAUNCH_CHECK();
 }
 

@@ -105,12 +105,7 @@ __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scal
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr k = from_mont(scalars[i]);
     canon[i] = k;
-    for (int l = 7; l >= 0; l--)
-      if (k.v[l]) {
-        unsigned bl = 32 * l + 32 - __builtin_clz(k.v[l]);
-        b = bl > b ? bl : b;
-        break;
-      }
+    b = max(b, fr_bit_length(k));
   }
   for (int o = 32; o > 0; o >>= 1) {
     unsigned x = __shfl_xor(b, o);
@@ -744,8 +739,16 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   (void)hipEventDestroy(ready);
   unsigned ba = 254, bb = 254;
   const Fr *ca = nullptr, *cb = nullptr;
-  if (a.n > 64) ca = bits_launch(l0, a.scalars, a.n);
-  if (b.n > 64) cb = bits_launch(l1, b.scalars, b.n);
+  // canonical inputs (the opening quotients) come with their bit lengths on the device
+  auto start = [&](MsmLane &ln, const MsmArgs &x) -> const Fr * {
+    if (x.n <= 64) return nullptr;
+    if (!x.canon_bits) return bits_launch(ln, x.scalars, x.n);
+    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
+                           ln.stream));
+    return x.scalars;
+  };
+  ca = start(l0, a);
+  cb = start(l1, b);
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
   MsmJob ja, jb;
