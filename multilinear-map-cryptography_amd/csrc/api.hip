@@ -844,7 +844,11 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
          &d_v = c->prove_ws[3], &d_o = c->prove_ws[4], &d_ca = c->prove_ws[5], &d_cv = c->prove_ws[6],
          &d_s = c->prove_ws[7];
-  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * L), *V = (Fr *)d_v.ensure(sizeof(Fr) * L), *O = (Fr *)d_o.ensure(sizeof(Fr) * L);
+  // V: a resident full slice is used in place (nothing below writes it); host input or a
+  // padded slice goes through the workspace
+  const bool v_in_place = kind == hipMemcpyDeviceToDevice && n_ops == L;
+  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * L), *O = (Fr *)d_o.ensure(sizeof(Fr) * L);
+  Fr *V = v_in_place ? (Fr *)const_cast<uint64_t *>(value) : (Fr *)d_v.ensure(sizeof(Fr) * L);
   const uint64_t *ar = addr;
   const uint8_t *fl = is_write;
   if (kind == hipMemcpyHostToDevice) {
@@ -857,7 +861,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     ar = dar;
     fl = dfl;
   }
-  if (n_ops) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
+  if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   fr_fill_zero_dev(c, A, L);
   to_mont_u64_dev(c, ar, A, n_ops);
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
@@ -866,7 +870,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   // ---- vector_to_polynomial + commit x2 (src/twist.rs:151-163).  The sum-check below
-  // folds A and V in place, so the openings work from copies of the evaluations.
+  // reads A and V without overwriting them, so the openings use the same vectors.
   Timer t_int;
   EvalPoly pa, pv;
   pa.N = pv.N = N;
@@ -874,11 +878,8 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   pa.cnt = pv.cnt = L;
   pa.coeffs = m.size == 1 ? (Fr *)d_ca.ensure(sizeof(Fr) * N) : nullptr;
   pv.coeffs = m.size == 1 ? (Fr *)d_cv.ensure(sizeof(Fr) * N) : nullptr;
-  Fr *YA = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * L), *YV = (Fr *)c->prove_ws[9].ensure(sizeof(Fr) * L);
-  TNS_HIP(hipMemcpyAsync(YA, A, sizeof(Fr) * L, hipMemcpyDeviceToDevice, st));
-  TNS_HIP(hipMemcpyAsync(YV, V, sizeof(Fr) * L, hipMemcpyDeviceToDevice, st));
-  pa.y = YA;
-  pv.y = YV;
+  pa.y = A;
+  pv.y = V;
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];
@@ -992,10 +993,8 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   pi.cnt = LM;
   pt.coeffs = m.size == 1 ? (Fr *)d_ct.ensure(sizeof(Fr) * T) : nullptr;
   pi.coeffs = m.size == 1 ? (Fr *)d_ci.ensure(sizeof(Fr) * M) : nullptr;
-  Fr *YI = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * LM);  // the sum-check folds I in place
-  TNS_HIP(hipMemcpyAsync(YI, I, sizeof(Fr) * LM, hipMemcpyDeviceToDevice, st));
   pt.y = TB;
-  pi.y = YI;
+  pi.y = I;  // the sum-check leaves its input tables intact (mle.hip)
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];

@@ -272,9 +272,36 @@ TNS_HD Fp<C> pow_u64(const Fp<C> &a, u64 e) {
   return acc;
 }
 
+#if defined(__HIPCC__)
+#include "inv_chain.inc"
+// Device Fermat inverse: a^(M-2) along a sliding-window (3-bit) addition chain over the constant
+// exponent (tools/gen_inv_chain.py: 62 window products for Fr, 56 for Fq, instead of the 127 /
+// 130 single-bit products of square-and-multiply), squarings with the dedicated lazy square,
+// everything in the lazy [0, 2M) domain until the final conditional subtraction.  The chain
+// is read from constant memory with a uniform index: the walk is uniform control flow.
+template <class C>
+__device__ __forceinline__ Fp<C> inv_window_dev(const Fp<C> &a) {
+  const Fp<C> a2 = sqr_lazy_dev(a);
+  const Fp<C> t1 = a, t3 = mul_lazy_dev(a, a2), t5 = mul_lazy_dev(t3, a2), t7 = mul_lazy_dev(t5, a2);
+  const unsigned char *steps = InvChain<C>::steps();
+  auto entry = [&](unsigned idx) -> const Fp<C> & { return idx == 0 ? t1 : idx == 1 ? t3 : idx == 2 ? t5 : t7; };
+  Fp<C> acc = entry(steps[0] & 3);
+  for (int k = 1; k < InvChain<C>::n; k++) {
+    const unsigned st = steps[k];
+    for (unsigned q = 0; q < (st >> 2); q++) acc = sqr_lazy_dev(acc);
+    acc = mul_lazy_dev(acc, entry(st & 3));
+  }
+  reduce_once(acc);  // lazy products of inputs < 2M stay < 2M
+  return acc;
+}
+#endif
+
 // Fermat inverse (a^(M-2)); inverse of zero is zero.
 template <class C>
 TNS_HD Fp<C> inv(const Fp<C> &a) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_MUL_CIOS)
+  return inv_window_dev(a);
+#endif
   u32 e[8];
   u64 br = 2;
 #pragma unroll

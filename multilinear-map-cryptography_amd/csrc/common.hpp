@@ -239,6 +239,7 @@ struct Ctx {
   std::mutex mu;
   // workspaces
   DevBuf scratch[8];
+  DevBuf sc_pong[4];    // sum-check: second fold buffer per table (the input tables stay intact)
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove

@@ -198,8 +198,8 @@ __global__ void __launch_bounds__(256) k_sum_partials4(const Fr *__restrict__ pa
 // a -> b -> a ...; out[i] = table i bound at all m challenges.  Replaces m - 1 small
 // k_sc_round launches and the k final k_mle_fold launches (each ~20 us of launch gap).
 struct ScTail {
-  Fr *a[MAX_SC_TABLES];
-  Fr *b[MAX_SC_TABLES];
+  const Fr *a[MAX_SC_TABLES];  // first input (may be the caller's table: only read)
+  Fr *b[MAX_SC_TABLES], *c[MAX_SC_TABLES];  // fold 0 -> b, then c, b, c, ...
 };
 constexpr unsigned SC_TAIL_LOG = 12;  // tables of <= 2^12 entries fold in the tail kernel
 
@@ -209,8 +209,8 @@ __global__ void __launch_bounds__(1024) k_sc_fold_tail(ScTail t, int k, int m, c
     const Fr r = ch[j];
     const unsigned half = 1u << (m - 1 - j);
     for (int i = 0; i < k; i++) {
-      const Fr *in = (j & 1) ? t.b[i] : t.a[i];
-      Fr *o = (j & 1) ? t.a[i] : t.b[i];
+      const Fr *in = j == 0 ? t.a[i] : (j & 1) ? t.b[i] : t.c[i];
+      Fr *o = (j & 1) ? t.c[i] : t.b[i];
       for (unsigned s = threadIdx.x; s < half; s += blockDim.x) {
         const Fr x0 = in[2 * s], x1 = in[2 * s + 1];
         o[s] = add(x0, mul(r, sub(x1, x0)));
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(1024) k_sc_fold_tail(ScTail t, int k, int m, c
     __syncthreads();  // fold j's outputs are fold j+1's inputs (other threads' entries)
   }
   if (threadIdx.x == 0)
-    for (int i = 0; i < k; i++) out[i] = ((m & 1) ? t.b[i] : t.a[i])[0];
+    for (int i = 0; i < k; i++) out[i] = ((m - 1) & 1 ? t.c[i] : t.b[i])[0];
 }
 
 static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n_terms) {
@@ -234,7 +234,7 @@ static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n
 }
 
 // SumCheck::prove (src/sumcheck.rs:56-110) for an MLE composition.
-// tables: k device arrays of 2^nv Fr (overwritten).  Host transcript drives challenges.
+// tables: k device arrays of 2^nv Fr (read only).  Host transcript drives challenges.
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_vals, Fr *final_eval) {
@@ -252,9 +252,14 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   }
   const bool has_terms = n_terms > 0;
   const size_t n = (size_t)1 << nv;
-  // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)).
-  Fr *bufB[MAX_SC_TABLES];
-  for (int i = 0; i < k; i++) bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
+  // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)); round 1
+  // reads the caller's tables, later rounds alternate between bufB and bufC, so the input
+  // tables are left intact (Twist / Shout open the same evaluation vectors afterwards).
+  Fr *bufB[MAX_SC_TABLES], *bufC[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
+    bufC[i] = (Fr *)c->sc_pong[i].ensure(sizeof(Fr) * (n / 4 + 1));
+  }
   const int nblk = (int)grid_for(n / 2 + 1, 256, 2048);
   Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * (size_t)nblk, 64));
   Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
@@ -291,9 +296,15 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
           k_sc_round<true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
         else
           k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-        // src now holds the freshly folded 2P-entry tables; the caller's tables
-        // become the next destination (they are consumed).
-        for (int i = 0; i < k; i++) std::swap(src[i], dst[i]);
+        // src now holds the freshly folded 2P-entry tables
+        for (int i = 0; i < k; i++) {
+          if (rnd == 1) {
+            src[i] = bufB[i];
+            dst[i] = bufC[i];
+          } else {
+            std::swap(src[i], dst[i]);
+          }
+        }
       }
       TNS_LAUNCH_CHECK();
     }
@@ -332,9 +343,10 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
     Fr *d_ch = partials, *d_out = sums_dev;
     TNS_HIP(hipMemcpyAsync(d_ch, tail_ch, sizeof(Fr) * m, hipMemcpyHostToDevice, c->stream));
     ScTail tl{};
-    for (int i = 0; i < k; i++) {
+    for (int i = 0; i < k; i++) {  // src may still be the caller's table (tail from round 1)
       tl.a[i] = src[i];
       tl.b[i] = dst[i];
+      tl.c[i] = src[i] == tables[i] ? bufC[i] : src[i];
     }
     TNS_PROF(c, "sumcheck_round", 96.0 * (double)(n >> (tail_rnd - 1)) * k);
     k_sc_fold_tail<<<1, 1024, 0, c->stream>>>(tl, k, m, d_ch, d_out);
