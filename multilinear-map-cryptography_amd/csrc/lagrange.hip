@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <tuple>
 #include <vector>
 
@@ -250,7 +251,14 @@ bool fr_is_node(const Fr &x, size_t N) {
   return v < N;
 }
 
-static size_t chain_count(size_t n) { return n < NODE_THREADS ? n : NODE_THREADS; }
+static size_t chain_count(size_t n) {
+  static const size_t T = [] {  // TNS_NODE_THREADS: tuning (power of two)
+    const char *e = getenv("TNS_NODE_THREADS");
+    const long v = e ? atol(e) : 0;
+    return v >= 256 && (v & (v - 1)) == 0 ? (size_t)v : (size_t)NODE_THREADS;
+  }();
+  return n < T ? n : T;
+}
 
 struct NodeSweep {
   size_t T;
