@@ -237,6 +237,9 @@ TNS_HD Fp<C> to_mont(const Fp<C> &canonical) {
 
 template <class C>
 TNS_HD Fp<C> from_mont(const Fp<C> &a) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_MUL_CIOS)
+  return redc_dev(a);  // the reduction alone: a * 1 needs no product columns
+#endif
   Fp<C> one = Fp<C>::zero();
   one.v[0] = 1;
   return mul(a, one);
