@@ -38,9 +38,14 @@ import numpy as np  # noqa: E402
 METRIC = "Twist prover ops/sec + KZG MSM G1-scalar-pairs/sec at 2^20, 1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # v_mad_u64_u32 throughput of independent streams, measured by tools/mulbench2.hip on MI355X
-# (profiles/r01_mulbench2.txt): the integer-VALU ceiling of the MSM accumulation.
+# (profiles/r01_mulbench2.txt): the integer-VALU ceiling of the MSM accumulation; and the
+# throughput of the mad + carry pairs each 32x32 MAC of the product needs (tools/macbench.hip,
+# 8 waves per SIMD, profiles/r02_macbench.txt).
 MAC_PEAK_T = 28.61
-MACS_PER_MADD = 10 * 128  # madd-2008-s: 10 Fq products of 8x8 32-bit limbs (+ as many for the reduction)
+MAC_PAIR_PEAK_T = 17.78
+# multiply-adds per lazy XYZZ mixed addition (bn254.hpp xyzz_madd_lazy): 6 products (64 + 64
+# reduction), 2 squares (36 + 64), Y3 as two products under one reduction (64 + 64 + 64)
+MACS_PER_MADD = 6 * 128 + 2 * 100 + 192
 
 
 def parse():
@@ -142,10 +147,13 @@ def roofline_from_profile(ts, ctx):
         tmacs = ex["ops"] * MACS_PER_MADD / (ex["busy_ms"] / 1e3) / 1e12
         roof["compute"] = {"kernel": "msm_accumulate", "bound": "valu (v_mad_u64_u32)", "unit": "T MAC/s",
                            "achieved": round(tmacs, 3), "peak": MAC_PEAK_T, "frac": round(tmacs / MAC_PEAK_T, 4),
+                           "mac_carry_pair_peak": MAC_PAIR_PEAK_T,
+                           "frac_of_pair_peak": round(tmacs / MAC_PAIR_PEAK_T, 4),
                            "madds": ex["ops"], "busy_ms": round(ex["busy_ms"], 3),
-                           "note": "mixed additions x 1280 MACs over the union of the stage's launch intervals; "
-                                   "peak = measured independent v_mad_u64_u32 streams (tools/mulbench2.hip); the "
-                                   "carry instruction of each MAC bounds the reachable fraction near 0.7"}
+                           "note": f"mixed additions x {MACS_PER_MADD} MACs over the union of the stage's launch "
+                                   "intervals; peak = measured independent v_mad_u64_u32 streams (tools/mulbench2.hip); "
+                                   "each MAC of the 32-bit-limb product also needs a carry instruction, and mad + carry "
+                                   "pairs peak at mac_carry_pair_peak (tools/macbench.hip, 8 waves/SIMD)"}
     return roof, stages
 
 
