@@ -14,7 +14,7 @@ import json
 import sys
 
 STAGES = {
-    "msm_digits": (["k_digits", "k_scalar_bits"], 4),
+    "msm_digits": (["k_digits", "k_scalar_bits"], 2),  # the commitments (openings arrive canonical)
     "msm_sort": (["rocprim", "k_bucket_bounds", "k_bs_"], 4),
     "msm_accumulate": (["k_accumulate"], 4),
     "msm_fixup": (["k_fix_level", "k_bucket_fixup"], 4),
