@@ -45,6 +45,7 @@ Ctx::~Ctx() {
   for (auto &kv : pass_tw) delete kv.second;
   for (auto &kv : bary_w) delete kv.second;
   if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
+  if (side) (void)hipStreamDestroy(side);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -331,6 +332,7 @@ int tns_ctx_create(int device, tns_ctx **out) {
     x->c.msm_cub_sort = cs && std::string(cs) == "cub";
     TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking,
                                         x->c.msm_stagger ? prio_hi : prio_lo));
+    TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
     *out = x;
     return TNS_OK;
   });
@@ -340,6 +342,7 @@ void tns_ctx_destroy(tns_ctx *ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->c.device);
   (void)hipStreamSynchronize(ctx->c.stream);
+  if (ctx->c.side) (void)hipStreamSynchronize(ctx->c.side);
   delete ctx;
 }
 
@@ -748,41 +751,39 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   unsigned lr = 0;
   while ((1 << lr) < m.size) lr++;
   const unsigned nv_loc = nv - lr;  // check_shard guarantees size <= 2^nv
-  std::vector<Fr> rounds(4 * (size_t)(nv ? nv : 1)), chal(nv ? nv : 1);
-  Fr finals[4], fe;
-  // zero constraint closure (src/twist.rs:186-214, src/shout.rs:160-184): no terms
-  sumcheck_prove_dev(c, mles, n_mles, nv_loc, Fr::zero(), nullptr, 0, tr, rounds.data(), chal.data(), finals, &fe);
-  if (lr) {
-    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles);  // rank-major
-    std::vector<std::vector<Fr>> tab(n_mles, std::vector<Fr>(m.size));
-    for (int r = 0; r < m.size; r++)
-      for (int j = 0; j < n_mles; j++) tab[j][r] = all[(size_t)r * n_mles + j];
-    char lab[64];
-    for (unsigned rnd = nv_loc; rnd < nv; rnd++) {
-      // round polynomial of the zero closure: [0, 0, 0, 0] (src/sumcheck.rs:77-96)
-      snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd);
-      tr.append_label(lab);
-      for (int x = 0; x < 4; x++) {
-        rounds[4 * rnd + x] = Fr::zero();
-        tr.append_fr(Fr::zero());
-      }
-      snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
-      const Fr ch = tr.challenge(lab);
-      chal[rnd] = ch;
-      for (auto &t : tab) {  // T'[s] = T[2s] + r (T[2s+1] - T[2s])
-        const size_t h = t.size() / 2;
-        for (size_t q = 0; q < h; q++) t[q] = add(t[2 * q], mul(ch, sub(t[2 * q + 1], t[2 * q])));
-        t.resize(h);
-      }
-    }
-    for (int j = 0; j < n_mles; j++) finals[j] = tab[j][0];
-    fe = Fr::zero();  // the closure is identically zero
+  if (n_mles < 1 || n_mles > 3) throw Error(TNS_ERR_INVALID_PARAMETERS, "1 to 3 trace tables");
+  // The zero constraint closure (src/twist.rs:186-214, src/shout.rs:160-184) makes every round
+  // polynomial [0, 0, 0, 0] and final_evaluation 0 (src/sumcheck.rs:77-104), so the transcript
+  // alone yields the challenges: all nv rounds run on the host first ...
+  const unsigned nv1 = nv ? nv : 1;
+  std::vector<Fr> rounds(4 * (size_t)nv1, Fr::zero());
+  Fr *chal = (Fr *)c->sc_host.ensure(sizeof(Fr) * (nv1 + 4)), *vals = chal + nv1;
+  char lab[64];
+  for (unsigned rnd = 0; rnd < nv; rnd++) {
+    snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd);  // src/sumcheck.rs:90-96
+    tr.append_label(lab);
+    for (int x = 0; x < 4; x++) tr.append_fr(Fr::zero());
+    snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
+    chal[rnd] = tr.challenge(lab);
   }
+  // ... and the folds binding this rank's tables at r_0 .. r_{nv_loc-1} (the MLE values the
+  // closure evaluates, src/sumcheck.rs:104) run on the side stream under the openings; their
+  // values are collected at the end of the proof
+  {
+    hipEvent_t ready;
+    TNS_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    TNS_HIP(hipEventRecord(ready, c->stream));  // the tables were written on the context stream
+    TNS_HIP(hipStreamWaitEvent(c->side, ready, 0));
+    (void)hipEventDestroy(ready);
+  }
+  Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
+  sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals);
+  TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
+  const Fr fe = Fr::zero();
   out->num_rounds = nv;
   std::memcpy(out->round_polynomials, rounds.data(), 128 * (size_t)nv);
-  std::memcpy(out->sumcheck_challenges, chal.data(), 32 * (size_t)nv);
+  std::memcpy(out->sumcheck_challenges, chal, 32 * (size_t)nv);
   std::memcpy(out->final_evaluation, &fe, 32);
-  for (int i = 0; i < n_mles && i < 3; i++) std::memcpy(out->final_mle_evals[i], &finals[i], 32);
   timing[3] = t_sc.ms();
   // challenge_field_elements("opening_challenges", nv) (src/utils.rs:195-203); only [0] used
   Timer t_open;
@@ -804,6 +805,25 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     out->num_openings = 2;
   }
   timing[4] = t_open.ms();
+  // the side stream's bound table values; with several ranks each holds its slice's values at
+  // r_0 .. r_{nv_loc-1}, and the last lr challenges fold the allgathered rank values
+  TNS_HIP(hipStreamSynchronize(c->side));
+  Fr finals[3];
+  for (int j = 0; j < n_mles; j++) finals[j] = vals[j];
+  if (lr) {
+    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles);  // rank-major
+    for (int j = 0; j < n_mles; j++) {
+      std::vector<Fr> t(m.size);
+      for (int r = 0; r < m.size; r++) t[r] = all[(size_t)r * n_mles + j];
+      for (unsigned rnd = nv_loc; rnd < nv; rnd++) {  // T'[s] = T[2s] + r (T[2s+1] - T[2s])
+        const size_t h = t.size() / 2;
+        for (size_t q = 0; q < h; q++) t[q] = add(t[2 * q], mul(chal[rnd], sub(t[2 * q + 1], t[2 * q])));
+        t.resize(h);
+      }
+      finals[j] = t[0];
+    }
+  }
+  for (int j = 0; j < n_mles; j++) std::memcpy(out->final_mle_evals[j], &finals[j], 32);
 }
 
 __global__ void k_write_flags(const uint8_t *__restrict__ in, Fr *__restrict__ out, size_t n_in, size_t n) {
@@ -839,6 +859,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     throw Error(TNS_ERR_INVALID_PARAMETERS, "local operation count does not match this rank's slice");
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
+  TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
   // ---- SoA extraction / padding into the resident workspace (src/twist.rs:115-148)
   Timer t_h2d;
   DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
@@ -951,6 +972,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     throw Error(TNS_ERR_INVALID_PARAMETERS, "local table / lookup count does not match this rank's slice");
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
+  TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
   Timer t_h2d;
   DevBuf &d_idx_raw = c->prove_ws[0], &d_bad = c->prove_ws[1], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3],
          &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];

@@ -240,6 +240,9 @@ struct Ctx {
   // workspaces
   DevBuf scratch[8];
   DevBuf sc_pong[4];    // sum-check: second fold buffer per table (the input tables stay intact)
+  DevBuf sc_half[4], sc_chal, sc_out;  // the zero-closure fold chain on the side stream
+  PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
+  hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
@@ -317,6 +320,8 @@ struct SumcheckTerm {
 // (consumed: they are folded in place into workspace).  Transcript callback is
 // host-side.  Returns status; fills rounds (nv x 4), challenges, final values.
 struct HostTranscript;
+void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
+                               Fr *d_out);
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_table_values, Fr *final_eval);

@@ -233,6 +233,67 @@ static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n
   return s;
 }
 
+// The zero-constraint sum-check of Twist / Shout (src/twist.rs:186-214, src/shout.rs:160-184):
+// every round polynomial is [0, 0, 0, 0], so the transcript alone yields the challenges and the
+// host has all of them before any fold runs.  The fold chain by those challenges is then pure
+// device work with no host wait: launched on `st` (a side stream) it runs under the openings,
+// and the k tables bound at every challenge land in d_out.  The input tables are only read.
+void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
+                               Fr *d_out) {
+  if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
+  if (nv == 0) {
+    for (int i = 0; i < k; i++) TNS_HIP(hipMemcpyAsync(d_out + i, tables[i], sizeof(Fr), hipMemcpyDeviceToDevice, st));
+    return;
+  }
+  const size_t n = (size_t)1 << nv;
+  Fr *bufB[MAX_SC_TABLES], *bufC[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    bufB[i] = (Fr *)c->sc_half[i].ensure(sizeof(Fr) * (n / 2 + 1));
+    bufC[i] = (Fr *)c->sc_pong[i].ensure(sizeof(Fr) * (n / 4 + 1));
+  }
+  Fr *d_ch = (Fr *)c->sc_chal.ensure(sizeof(Fr) * nv);
+  TNS_HIP(hipMemcpyAsync(d_ch, chal_pinned, sizeof(Fr) * nv, hipMemcpyHostToDevice, st));
+  // rounds 1 .. tail_rnd - 1 fold by r_{rnd-1} in k_sc_round; the rest (tables of <= 2^12) in
+  // one k_sc_fold_tail workgroup, down to one value per table
+  const unsigned tail_rnd = std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG));
+  Fr *src[MAX_SC_TABLES], *dst[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    src[i] = tables[i];
+    dst[i] = bufB[i];
+  }
+  Fr ch[64];
+  std::memcpy(ch, chal_pinned, sizeof(Fr) * std::min(nv, 64u));
+  for (unsigned rnd = 1; rnd < tail_rnd; rnd++) {
+    const size_t P = n >> (rnd + 1);
+    ScTables tt{};
+    for (int i = 0; i < k; i++) {
+      tt.in[i] = src[i];
+      tt.out[i] = dst[i];
+    }
+    TNS_PROF_ON(c, st, "sumcheck_round", 192.0 * (double)P * k);
+    k_sc_round<true, false><<<grid_for(P, 256, 2048), 256, 0, st>>>(tt, k, ScTerms{}, P, ch[rnd - 1], nullptr);
+    TNS_LAUNCH_CHECK();
+    for (int i = 0; i < k; i++) {
+      if (rnd == 1) {
+        src[i] = bufB[i];
+        dst[i] = bufC[i];
+      } else {
+        std::swap(src[i], dst[i]);
+      }
+    }
+  }
+  ScTail tl{};
+  for (int i = 0; i < k; i++) {
+    tl.a[i] = src[i];
+    tl.b[i] = dst[i];
+    tl.c[i] = src[i] == tables[i] ? bufC[i] : src[i];
+  }
+  const int m = (int)(nv - tail_rnd + 1);
+  TNS_PROF_ON(c, st, "sumcheck_round", 96.0 * (double)(n >> (tail_rnd - 1)) * k);
+  k_sc_fold_tail<<<1, 1024, 0, st>>>(tl, k, m, d_ch + (tail_rnd - 1), d_out);
+  TNS_LAUNCH_CHECK();
+}
+
 // SumCheck::prove (src/sumcheck.rs:56-110) for an MLE composition.
 // tables: k device arrays of 2^nv Fr (read only).  Host transcript drives challenges.
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
