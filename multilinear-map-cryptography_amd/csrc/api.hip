@@ -200,18 +200,30 @@ static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affin
   out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 1));
 }
 
-static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, Comm &m, G1Affine out[2]) {
+// src0 / src1 (optional): how p0.y / p1.y get written (on the MSM lane that reads them)
+static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, Comm &m, G1Affine out[2],
+                              const ScalarSource *src0 = nullptr, const ScalarSource *src1 = nullptr) {
   if (p0.N > srs.n || p1.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
   p0.basis = lagrange_basis_dev(c, srs, p0.N, p0.first, p0.cnt);
   p1.basis = lagrange_basis_dev(c, srs, p1.N, p1.first, p1.cnt);
   if (!p0.basis || !p1.basis) {
+    for (const ScalarSource *s : {src0, src1})
+      if (s && s->prep) s->prep(c->stream);
     out[0] = commit_evals(c, srs, p0, m);
     out[1] = commit_evals(c, srs, p1, m);
     return;
   }
+  auto args = [](const EvalPoly &p, const ScalarSource *s) {
+    MsmArgs a{p.basis->points.as<G1Affine>(), p.y, p.cnt, p.basis->fb};
+    if (s) {
+      a.prep = s->prep;
+      a.canon = s->canon;
+      a.canon_bits = s->canon_bits;
+    }
+    return a;
+  };
   G1Xyzz part[2];
-  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), p0.y, p0.cnt, p0.basis->fb},
-               MsmArgs{p1.basis->points.as<G1Affine>(), p1.y, p1.cnt, p1.basis->fb}, part);
+  msm_pair_dev(c, args(p0, src0), args(p1, src1), part);
   allgather_sum_g1_pair(c, m, part, out);
 }
 
@@ -883,13 +895,28 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     fl = dfl;
   }
   if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
-  fr_fill_zero_dev(c, A, L);
-  to_mont_u64_dev(c, ar, A, n_ops);
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
-  k_write_flags<<<grid_for(L, 256), 256, 0, st>>>(fl, O, n_ops, L);
+  // the op-type table is read by the sum-check only: written on the side stream
+  {
+    hipEvent_t in_ready;
+    TNS_HIP(hipEventCreateWithFlags(&in_ready, hipEventDisableTiming));
+    TNS_HIP(hipEventRecord(in_ready, st));
+    TNS_HIP(hipStreamWaitEvent(c->side, in_ready, 0));
+    (void)hipEventDestroy(in_ready);
+  }
+  k_write_flags<<<grid_for(L, 256), 256, 0, c->side>>>(fl, O, n_ops, L);
   TNS_LAUNCH_CHECK();
-  TNS_HIP(hipStreamSynchronize(st));
+  if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
+  // the address table (Montgomery for the sum-check and the openings, canonical with its bit
+  // length for the commitment's sort) is written on lane 0 as its MSM starts, so the value
+  // commitment's lane does not wait for it
+  Fr *A_canon = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * L);
+  unsigned *a_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
+  ScalarSource src_a;
+  src_a.prep = [=](hipStream_t s) { u64_tables_dev(s, ar, n_ops, L, A, A_canon, a_bits); };
+  src_a.canon = A_canon;
+  src_a.canon_bits = a_bits;
   // ---- vector_to_polynomial + commit x2 (src/twist.rs:151-163).  The sum-check below
   // reads A and V without overwriting them, so the openings use the same vectors.
   Timer t_int;
@@ -904,7 +931,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];
-  commit_evals_pair(c, srs->s, pa, pv, m, cm);
+  commit_evals_pair(c, srs->s, pa, pv, m, cm, &src_a, nullptr);
   const G1Affine Ca = cm[0], Cv = cm[1];
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
@@ -978,7 +1005,6 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
          &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
   Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * LT), *I = (Fr *)d_i.ensure(sizeof(Fr) * LM);
   fr_fill_zero_dev(c, TB, LT);
-  fr_fill_zero_dev(c, I, LM);
   if (n_entries) TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
   // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
   unsigned hbad = 0;
@@ -1002,9 +1028,15 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     for (unsigned f : flags) hbad |= f;
   }
   if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
-  if (n_lookups) to_mont_u64_dev(c, ir, I, n_lookups);
-  TNS_HIP(hipStreamSynchronize(st));
+  if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
+  // the index table is written on lane 1 as the index commitment starts (see twist_core)
+  Fr *I_canon = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * LM);
+  unsigned *i_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
+  ScalarSource src_i;
+  src_i.prep = [=](hipStream_t s) { u64_tables_dev(s, ir, n_lookups, LM, I, I_canon, i_bits); };
+  src_i.canon = I_canon;
+  src_i.canon_bits = i_bits;
   Timer t_int;
   EvalPoly pt, pi;
   pt.N = T;
@@ -1020,7 +1052,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];
-  commit_evals_pair(c, srs->s, pt, pi, m, cm);  // table first (src/shout.rs:125-133)
+  commit_evals_pair(c, srs->s, pt, pi, m, cm, nullptr, &src_i);  // table first (src/shout.rs:125-133)
   const G1Affine Ct = cm[0], Ci = cm[1];
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);

@@ -7,6 +7,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <stdexcept>
@@ -331,8 +332,10 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
 Fr synthetic_division_dev(Ctx *c, const Fr *coeffs, size_t n, const Fr &z, Fr *q);
 // g1_powers[first .. first + n) = G * tau^i
 void srs_generate_dev(Ctx *c, const Fr &tau, size_t first, size_t n, G1Affine *out);
-void to_mont_u64_dev(Ctx *c, const uint64_t *in, Fr *out, size_t n);
 void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
+// u64 entries [0, n_in) zero-padded to n: Montgomery form (mont), canonical form (canon)
+// and the largest bit length (*bits, zeroed here) in one pass on stream s
+void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
 G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr);
@@ -349,8 +352,19 @@ struct MsmArgs {
   const Fr *scalars;
   size_t n;
   const FixedBase *fb;
-  // set: `scalars` are CANONICAL (not Montgomery) and their largest bit length is at this
-  // device address (n > 64 only: the tiny path reads Montgomery scalars)
+  // set: the scalars' largest bit length is at this device address and the sort reads
+  // canonical scalars -- `canon` if set (then `scalars` stay Montgomery, for the tiny path),
+  // else `scalars` themselves (n > 64 only: the tiny path reads Montgomery scalars)
+  const unsigned *canon_bits = nullptr;
+  const Fr *canon = nullptr;
+  // enqueued on the lane's stream before anything else of this MSM: produces the scalars
+  // (and canon / canon_bits) without holding up the other lane
+  std::function<void(hipStream_t)> prep;
+};
+// how one vector of commit_evals_pair gets ready (the MsmArgs fields of the same names)
+struct ScalarSource {
+  std::function<void(hipStream_t)> prep;
+  const Fr *canon = nullptr;
   const unsigned *canon_bits = nullptr;
 };
 // two independent MSMs overlapped on the context's two lanes (inputs ready on c->stream)

@@ -66,7 +66,10 @@ static double plan_cost(size_t n, int W, int c, int sets) {
   return (double)W * (double)n + 3.0 * sets * (double)((size_t)1 << (c - 1));
 }
 
-static int best_window(size_t n, int bits, int cmax, bool shared) {
+// w1max > cmax: scalars of up to w1max - 1 bits may also take one window of bits + 1 (no
+// second window for the signed digits' carry, e.g. 22-bit trace addresses: n additions
+// instead of 2n, and no thousands-deep buckets)
+static int best_window(size_t n, int bits, int cmax, bool shared, int w1max = 0) {
   int lg = 0;
   while (((size_t)1 << lg) < n) lg++;
   double best = 1e300;
@@ -79,6 +82,8 @@ static int best_window(size_t n, int bits, int cmax, bool shared) {
       bc = c;
     }
   }
+  const int c1 = bits + 1;
+  if (c1 > cmax && c1 <= w1max && c1 <= lg + 2 && plan_cost(n, 1, c1, 1) < best * 0.98) bc = c1;
   return bc;
 }
 
@@ -521,7 +526,8 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   // plan: per-window layout, or the shared layout when a fixed-base table covers the points
   MsmPlan &P = J.P;
   P = MsmPlan();
-  P.c = best_window(n, (int)bits, 20, false);
+  const char *w1 = getenv("TNS_MSM_W1");  // =0: no single-window plan (A/B, tests)
+  P.c = best_window(n, (int)bits, 20, false, w1 && w1[0] == '0' ? 0 : 23);
   if (ctx->msm_c >= 4) P.c = ctx->msm_c;
   P.W = windows_for((int)bits, P.c);
   if (fb && ctx->msm_tables && fb->n >= n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
@@ -741,11 +747,12 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   const Fr *ca = nullptr, *cb = nullptr;
   // canonical inputs (the opening quotients) come with their bit lengths on the device
   auto start = [&](MsmLane &ln, const MsmArgs &x) -> const Fr * {
+    if (x.prep) x.prep(ln.stream);
     if (x.n <= 64) return nullptr;
     if (!x.canon_bits) return bits_launch(ln, x.scalars, x.n);
     TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
                            ln.stream));
-    return x.scalars;
+    return x.canon ? x.canon : x.scalars;
   };
   ca = start(l0, a);
   cb = start(l1, b);

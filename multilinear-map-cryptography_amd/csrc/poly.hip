@@ -91,14 +91,29 @@ Fr synthetic_division_dev(Ctx *ctx, const Fr *coeffs, size_t n, const Fr &z, Fr 
 }
 
 // ---------------------------------------------------------------- conversions
-__global__ void k_to_mont_u64(const uint64_t *__restrict__ in, Fr *__restrict__ out, size_t n) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x)
-    out[i] = from_u64<FrCfg>(in[i]);
+__global__ void __launch_bounds__(256) k_u64_tables(const uint64_t *__restrict__ in, size_t n_in, size_t n,
+                                                    Fr *__restrict__ mont, Fr *__restrict__ canon,
+                                                    unsigned *__restrict__ bits) {
+  unsigned b = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const uint64_t x = i < n_in ? in[i] : 0;
+    Fr k = Fr::zero();
+    k.v[0] = (uint32_t)x;
+    k.v[1] = (uint32_t)(x >> 32);
+    canon[i] = k;
+    mont[i] = from_u64<FrCfg>(x);
+    b = x ? max(b, 64u - (unsigned)__builtin_clzll(x)) : b;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned y = __shfl_xor(b, o);
+    b = y > b ? y : b;
+  }
+  if ((threadIdx.x & 63) == 0 && b) atomicMax(bits, b);
 }
-void to_mont_u64_dev(Ctx *c, const uint64_t *in, Fr *out, size_t n) {
+void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits) {
+  TNS_HIP(hipMemsetAsync(bits, 0, sizeof(unsigned), s));
   if (!n) return;
-  k_to_mont_u64<<<grid_for(n, 256), 256, 0, c->stream>>>(in, out, n);
+  k_u64_tables<<<grid_for(n, 256), 256, 0, s>>>(in, n_in, n, mont, canon, bits);
   TNS_LAUNCH_CHECK();
 }
 void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n) {
