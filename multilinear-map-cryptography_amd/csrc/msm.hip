@@ -167,6 +167,27 @@ __global__ void __launch_bounds__(256) k_bucket_bounds(const uint32_t *__restric
   }
 }
 
+// A/B builds only (tools/build_variant.sh): -DTNS_ACC_PTMASK=0xffff gathers every point from a
+// 4 MB slice (L2-resident; wrong sums) to separate the gather's cost from the arithmetic's
+#ifndef TNS_ACC_PTMASK
+#define TNS_ACC_PTMASK 0x7fffffffu
+#endif
+
+// the accumulation's point gather (TNS_ACC_NT=1 A/B build: non-temporal loads)
+typedef uint32_t acc_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ G1Affine load_point(const G1Affine *__restrict__ pts, uint32_t i) {
+#if defined(TNS_ACC_NT) && TNS_ACC_NT
+  const acc_v4u *s = reinterpret_cast<const acc_v4u *>(pts + i);
+  G1Affine q;
+  acc_v4u *d = reinterpret_cast<acc_v4u *>(&q);
+#pragma unroll
+  for (int k = 0; k < 4; k++) d[k] = __builtin_nontemporal_load(s + k);
+  return q;
+#else
+  return pts[i];
+#endif
+}
+
 struct HeadTail {
   G1Xyzz head, tail;
 };
@@ -203,7 +224,7 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
       // (gathering entry p + 1 ahead of this addition measured no faster: 39.48 vs 39.46 ms of
       // accumulation per C4 step -- three waves per SIMD hide the gather)
       const uint32_t v = vals[p];
-      G1Affine q = pts[v & 0x7fffffffu];
+      G1Affine q = load_point(pts, v & TNS_ACC_PTMASK);
       const Fq ny = sub_dev(Fq::zero(), q.y);  // -y (0 stays 0: the identity is (0, 0))
 #pragma unroll
       for (int l = 0; l < 8; l++) q.y.v[l] = (v >> 31) ? ny.v[l] : q.y.v[l];
