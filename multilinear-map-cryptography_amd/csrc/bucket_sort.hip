@@ -29,7 +29,10 @@
 
 namespace tns {
 
-constexpr int BS_BLOCK = 256;  // 4 waves: fits the slots k_accumulate leaves free
+#ifndef TNS_BS_BLOCK
+#define TNS_BS_BLOCK 256
+#endif
+constexpr int BS_BLOCK = TNS_BS_BLOCK;  // 4 waves: fits the slots k_accumulate leaves free
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
 constexpr int BS_TILE = 8192;  // entries per tile at most (LDS staging: 64 KiB)
