@@ -238,6 +238,27 @@ static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n
 // host has all of them before any fold runs.  The fold chain by those challenges is then pure
 // device work with no host wait: launched on `st` (a side stream) it runs under the openings,
 // and the k tables bound at every challenge land in d_out.  The input tables are only read.
+// three zero-closure folds in one pass (challenges r0, r1, r2 of consecutive rounds): out[s] from
+// in[8s .. 8s + 7] -- one read of the tables per three rounds instead of per round
+__global__ void __launch_bounds__(256) k_sc_fold3(ScTables t, int k, size_t P, Fr r0, Fr r1, Fr r2) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int i = 0; i < MAX_SC_TABLES; i++) {
+      if (i < k) {
+        const Fr *p = t.in[i] + 8 * s;
+        Fr x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = p[j];
+        Fr a[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) a[j] = add(x[2 * j], mul(r0, sub(x[2 * j + 1], x[2 * j])));
+        const Fr b0 = add(a[0], mul(r1, sub(a[1], a[0]))), b1 = add(a[2], mul(r1, sub(a[3], a[2])));
+        t.out[i][s] = add(b0, mul(r2, sub(b1, b0)));
+      }
+    }
+  }
+}
+
 void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
                                Fr *d_out) {
   if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
@@ -263,18 +284,29 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   }
   Fr ch[64];
   std::memcpy(ch, chal_pinned, sizeof(Fr) * std::min(nv, 64u));
-  for (unsigned rnd = 1; rnd < tail_rnd; rnd++) {
-    const size_t P = n >> (rnd + 1);
+  const char *f3 = getenv("TNS_SC_FOLD3");  // =0: one launch per round (A/B)
+  const bool fold3 = !(f3 && f3[0] == '0');
+  for (unsigned rnd = 1; rnd < tail_rnd;) {
     ScTables tt{};
     for (int i = 0; i < k; i++) {
       tt.in[i] = src[i];
       tt.out[i] = dst[i];
     }
-    TNS_PROF_ON(c, st, "sumcheck_round", 192.0 * (double)P * k);
-    k_sc_round<true, false><<<grid_for(P, 256, 2048), 256, 0, st>>>(tt, k, ScTerms{}, P, ch[rnd - 1], nullptr);
-    TNS_LAUNCH_CHECK();
+    if (fold3 && rnd + 2 < tail_rnd) {  // rounds rnd .. rnd + 2 in one pass
+      const size_t P = n >> (rnd + 2);
+      TNS_PROF_ON(c, st, "sumcheck_round", 288.0 * (double)P * k);
+      k_sc_fold3<<<grid_for(P, 256, 4096), 256, 0, st>>>(tt, k, P, ch[rnd - 1], ch[rnd], ch[rnd + 1]);
+      TNS_LAUNCH_CHECK();
+      rnd += 3;
+    } else {
+      const size_t P = n >> (rnd + 1);
+      TNS_PROF_ON(c, st, "sumcheck_round", 192.0 * (double)P * k);
+      k_sc_round<true, false><<<grid_for(P, 256, 2048), 256, 0, st>>>(tt, k, ScTerms{}, P, ch[rnd - 1], nullptr);
+      TNS_LAUNCH_CHECK();
+      rnd += 1;
+    }
     for (int i = 0; i < k; i++) {
-      if (rnd == 1) {
+      if (src[i] == tables[i]) {  // after the first pass: bufB holds the tables' fold
         src[i] = bufB[i];
         dst[i] = bufC[i];
       } else {

@@ -476,8 +476,9 @@ def _check_twist_properties(pp, addr, val_mont, isw, pr):
 
 
 # 10: the whole fold chain runs in k_sc_fold_tail; 13 / 14: one / two k_sc_round folds first
-# (the tail then starts from the scratch / the caller's buffers)
-@pytest.mark.parametrize("logn", [10, 13, 14])
+# (the tail then starts from the scratch / the caller's buffers); 15 / 16: one three-round
+# k_sc_fold3 pass (then nothing / one k_sc_round) before the tail
+@pytest.mark.parametrize("logn", [10, 13, 14, 15, 16])
 def test_twist_bench_trace_properties(logn):
     L = logn - 2
     pp, _ = params(L)
