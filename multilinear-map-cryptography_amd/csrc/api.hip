@@ -756,9 +756,10 @@ int tns_last_prove_timing(tns_ctx *ctx, double out_ms[6]) {
 // The first nv - log2(size) rounds bind variables inside every slice (LSB-first,
 // src/polynomials.rs:111-119), so they run locally; the last log2(size) rounds run on
 // the host over the one folded value per table and rank (allgathered).
+// flags (optional): the last of the mles as 0/1 bytes (sumcheck_zero_folds_async)
 static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *const *mles, int n_mles,
                              unsigned nv, EvalPoly &polyA, EvalPoly &polyB, tns_proof *out, double *timing,
-                             DevBuf &sbuf, Comm &m) {
+                             DevBuf &sbuf, Comm &m, const uint8_t *flags = nullptr, size_t n_flags = 0) {
   Timer t_sc;
   unsigned lr = 0;
   while ((1 << lr) < m.size) lr++;
@@ -789,7 +790,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     (void)hipEventDestroy(ready);
   }
   Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
-  sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals);
+  sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals, flags, n_flags);
   TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
   const Fr fe = Fr::zero();
   out->num_rounds = nv;
@@ -880,7 +881,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   // V: a resident full slice is used in place (nothing below writes it); host input or a
   // padded slice goes through the workspace
   const bool v_in_place = kind == hipMemcpyDeviceToDevice && n_ops == L;
-  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * L), *O = (Fr *)d_o.ensure(sizeof(Fr) * L);
+  Fr *A = (Fr *)d_a.ensure(sizeof(Fr) * L), *O = nullptr;
   Fr *V = v_in_place ? (Fr *)const_cast<uint64_t *>(value) : (Fr *)d_v.ensure(sizeof(Fr) * L);
   const uint64_t *ar = addr;
   const uint8_t *fl = is_write;
@@ -896,16 +897,21 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   }
   if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
-  // the op-type table is read by the sum-check only: written on the side stream
-  {
+  // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
+  // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
+  unsigned lr = 0;
+  while ((1 << lr) < m.size) lr++;
+  const bool flag_bytes = sumcheck_folds_take_flag_bytes(nv - lr);
+  if (!flag_bytes) {
+    O = (Fr *)d_o.ensure(sizeof(Fr) * L);
     hipEvent_t in_ready;
     TNS_HIP(hipEventCreateWithFlags(&in_ready, hipEventDisableTiming));
     TNS_HIP(hipEventRecord(in_ready, st));
     TNS_HIP(hipStreamWaitEvent(c->side, in_ready, 0));
     (void)hipEventDestroy(in_ready);
+    k_write_flags<<<grid_for(L, 256), 256, 0, c->side>>>(fl, O, n_ops, L);
+    TNS_LAUNCH_CHECK();
   }
-  k_write_flags<<<grid_for(L, 256), 256, 0, c->side>>>(fl, O, n_ops, L);
-  TNS_LAUNCH_CHECK();
   if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   // the address table (Montgomery for the sum-check and the openings, canonical with its bit
@@ -944,7 +950,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tr.append_fr(commitment_hash(Cv));
   // ---- sum-check over the addr / value / op-type MLEs + openings (src/twist.rs:177-243)
   Fr *mles[3] = {A, V, O};
-  fill_common_tail(c, srs->s, tr, mles, 3, nv, pa, pv, out, tm, d_s, m);
+  fill_common_tail(c, srs->s, tr, mles, 3, nv, pa, pv, out, tm, d_s, m, flag_bytes ? fl : nullptr, n_ops);
   TNS_HIP(hipStreamSynchronize(st));
   tm[5] = total.ms();
 }

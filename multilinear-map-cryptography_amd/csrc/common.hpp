@@ -321,8 +321,12 @@ struct SumcheckTerm {
 // (consumed: they are folded in place into workspace).  Transcript callback is
 // host-side.  Returns status; fills rounds (nv x 4), challenges, final values.
 struct HostTranscript;
+// The zero-closure fold chain (mle.hip): binds the k tables at the challenges on stream st and
+// writes their values to d_out.  flags (optional): the last table as 0/1 bytes (n_flags of
+// them, zero beyond), tables[k - 1] unused -- only when sumcheck_folds_take_flag_bytes(nv).
+bool sumcheck_folds_take_flag_bytes(unsigned nv);
 void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
-                               Fr *d_out);
+                               Fr *d_out, const uint8_t *flags = nullptr, size_t n_flags = 0);
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_table_values, Fr *final_eval);

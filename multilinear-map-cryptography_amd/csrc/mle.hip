@@ -240,18 +240,42 @@ static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n
 // and the k tables bound at every challenge land in d_out.  The input tables are only read.
 // three zero-closure folds in one pass (challenges r0, r1, r2 of consecutive rounds): out[s] from
 // in[8s .. 8s + 7] -- one read of the tables per three rounds instead of per round
-__global__ void __launch_bounds__(256) k_sc_fold3(ScTables t, int k, size_t P, Fr r0, Fr r1, Fr r2) {
+// flags (optional): the last table is 0/1 flags given as bytes (entries >= n_flags are 0), so its
+// first fold is a select among 0, 1, r0 and 1 - r0 -- the table itself never exists
+__global__ void __launch_bounds__(256) k_sc_fold3(ScTables t, int k, size_t P, Fr r0, Fr r1, Fr r2,
+                                                  const uint8_t *__restrict__ flags, size_t n_flags) {
+  const Fr one = Fr::one(), omr = sub(Fr::one(), r0);
   for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int i = 0; i < MAX_SC_TABLES; i++) {
       if (i < k) {
-        const Fr *p = t.in[i] + 8 * s;
-        Fr x[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) x[j] = p[j];
         Fr a[4];
+        if (flags && i == k - 1) {
+          uint32_t f[8];
+          if (8 * s + 8 <= n_flags && ((uintptr_t)flags & 7) == 0) {
+            const uint2 w = *reinterpret_cast<const uint2 *>(flags + 8 * s);  // 8-byte aligned
 #pragma unroll
-        for (int j = 0; j < 4; j++) a[j] = add(x[2 * j], mul(r0, sub(x[2 * j + 1], x[2 * j])));
+            for (int j = 0; j < 4; j++) {
+              f[j] = (w.x >> (8 * j)) & 0xff;
+              f[4 + j] = (w.y >> (8 * j)) & 0xff;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) f[j] = 8 * s + j < n_flags ? flags[8 * s + j] : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const bool f0 = f[2 * j] != 0, f1 = f[2 * j + 1] != 0;  // f0 + r0 (f1 - f0)
+            a[j] = f0 ? (f1 ? one : omr) : (f1 ? r0 : Fr::zero());
+          }
+        } else {
+          const Fr *p = t.in[i] + 8 * s;
+          Fr x[8];
+#pragma unroll
+          for (int j = 0; j < 8; j++) x[j] = p[j];
+#pragma unroll
+          for (int j = 0; j < 4; j++) a[j] = add(x[2 * j], mul(r0, sub(x[2 * j + 1], x[2 * j])));
+        }
         const Fr b0 = add(a[0], mul(r1, sub(a[1], a[0]))), b1 = add(a[2], mul(r1, sub(a[3], a[2])));
         t.out[i][s] = add(b0, mul(r2, sub(b1, b0)));
       }
@@ -259,9 +283,20 @@ __global__ void __launch_bounds__(256) k_sc_fold3(ScTables t, int k, size_t P, F
   }
 }
 
+static bool sc_fold3_on() {
+  const char *f3 = getenv("TNS_SC_FOLD3");  // =0: one launch per round (A/B)
+  return !(f3 && f3[0] == '0');
+}
+
+static unsigned sc_tail_round(unsigned nv) { return std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG)); }
+
+bool sumcheck_folds_take_flag_bytes(unsigned nv) { return sc_fold3_on() && sc_tail_round(nv) > 3; }
+
 void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
-                               Fr *d_out) {
+                               Fr *d_out, const uint8_t *flags, size_t n_flags) {
   if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
+  if (flags && !sumcheck_folds_take_flag_bytes(nv))
+    throw Error(TNS_ERR_SUMCHECK, "flag bytes need a first three-round fold pass");
   if (nv == 0) {
     for (int i = 0; i < k; i++) TNS_HIP(hipMemcpyAsync(d_out + i, tables[i], sizeof(Fr), hipMemcpyDeviceToDevice, st));
     return;
@@ -276,7 +311,7 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   TNS_HIP(hipMemcpyAsync(d_ch, chal_pinned, sizeof(Fr) * nv, hipMemcpyHostToDevice, st));
   // rounds 1 .. tail_rnd - 1 fold by r_{rnd-1} in k_sc_round; the rest (tables of <= 2^12) in
   // one k_sc_fold_tail workgroup, down to one value per table
-  const unsigned tail_rnd = std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG));
+  const unsigned tail_rnd = sc_tail_round(nv);
   Fr *src[MAX_SC_TABLES], *dst[MAX_SC_TABLES];
   for (int i = 0; i < k; i++) {
     src[i] = tables[i];
@@ -284,8 +319,8 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   }
   Fr ch[64];
   std::memcpy(ch, chal_pinned, sizeof(Fr) * std::min(nv, 64u));
-  const char *f3 = getenv("TNS_SC_FOLD3");  // =0: one launch per round (A/B)
-  const bool fold3 = !(f3 && f3[0] == '0');
+  const bool fold3 = sc_fold3_on();
+  bool first = true;
   for (unsigned rnd = 1; rnd < tail_rnd;) {
     ScTables tt{};
     for (int i = 0; i < k; i++) {
@@ -295,7 +330,8 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
     if (fold3 && rnd + 2 < tail_rnd) {  // rounds rnd .. rnd + 2 in one pass
       const size_t P = n >> (rnd + 2);
       TNS_PROF_ON(c, st, "sumcheck_round", 288.0 * (double)P * k);
-      k_sc_fold3<<<grid_for(P, 256, 4096), 256, 0, st>>>(tt, k, P, ch[rnd - 1], ch[rnd], ch[rnd + 1]);
+      k_sc_fold3<<<grid_for(P, 256, 4096), 256, 0, st>>>(tt, k, P, ch[rnd - 1], ch[rnd], ch[rnd + 1],
+                                                          first ? flags : nullptr, n_flags);
       TNS_LAUNCH_CHECK();
       rnd += 3;
     } else {
@@ -306,19 +342,20 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
       rnd += 1;
     }
     for (int i = 0; i < k; i++) {
-      if (src[i] == tables[i]) {  // after the first pass: bufB holds the tables' fold
+      if (first) {  // after the first pass: bufB holds the tables' fold
         src[i] = bufB[i];
         dst[i] = bufC[i];
       } else {
         std::swap(src[i], dst[i]);
       }
     }
+    first = false;
   }
   ScTail tl{};
   for (int i = 0; i < k; i++) {
     tl.a[i] = src[i];
     tl.b[i] = dst[i];
-    tl.c[i] = src[i] == tables[i] ? bufC[i] : src[i];
+    tl.c[i] = first ? bufC[i] : src[i];
   }
   const int m = (int)(nv - tail_rnd + 1);
   TNS_PROF_ON(c, st, "sumcheck_round", 96.0 * (double)(n >> (tail_rnd - 1)) * k);

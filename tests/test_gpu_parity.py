@@ -491,6 +491,24 @@ def test_twist_bench_trace_properties(logn):
     assert pr.final_mle_evals == want
 
 
+@pytest.mark.parametrize("n_ops", [(1 << 15) + 1, (1 << 16) - 13])
+def test_twist_ragged_fold_chain_from_flag_bytes(n_ops):
+    """From 2^15 padded operations the op-type table's first fold reads the is_write bytes (zero
+    beyond the trace, an unaligned tail); the bound values still equal the padded tables' MLEs."""
+    n = 1 << (n_ops - 1).bit_length()
+    L = n.bit_length() - 3
+    pp, _ = params(L)
+    addr, val, isw = ts.bench_trace(1 << L, n_ops)
+    pr = ts.Twist(pp).prove_soa(addr, val, isw)
+    chals = _check_twist_properties(pp, addr, val, isw, pr)
+    pad = n - n_ops
+    cols = (np.concatenate([addr, np.zeros(pad, np.uint64)]), np.concatenate([val, np.zeros((pad, 4), np.uint64)]),
+            np.concatenate([isw.astype(np.uint64), np.zeros(pad, np.uint64)]))
+    want = [co.fr_ints(co.mle_evaluate(t, ts.to_mont(chals)))[0]
+            for t in (ts.fr_from_u64_array(cols[0]), cols[1], ts.fr_from_u64_array(cols[2]))]
+    assert pr.final_mle_evals == want
+
+
 def test_twist_ragged_trace_properties():
     pp, _ = params(8)  # max_operations 1024
     addr, val, isw = ts.bench_trace(256, 1000)  # pads to 1024
