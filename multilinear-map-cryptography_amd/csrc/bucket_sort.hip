@@ -515,7 +515,7 @@ static int pass_tile(int p) {
 // [bstart[b], bstart[b+1]), b < 2^bucket_bits) and the shift from key to bucket;
 // *valid = number of entries (non-zero digits).
 BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
-                            int bucket_bits, uint32_t *valid) {
+                            int bucket_bits, uint32_t *valid, std::function<void()> *before_sync) {
   hipStream_t st = ln.stream;
   const size_t E = (size_t)W * n;
   if (E >= ((size_t)1 << 32)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one bucket sort");
@@ -607,6 +607,11 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
       uint32_t *h = (uint32_t *)ln.host2.ensure(2 * sizeof(uint32_t));
       TNS_HIP(hipMemcpyAsync(h, tbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       TNS_HIP(hipMemcpyAsync(h + 1, mbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      if (before_sync && *before_sync) {  // e.g. the other lane's sort, enqueued before this wait
+        auto f = std::move(*before_sync);
+        *before_sync = nullptr;
+        f();
+      }
       TNS_HIP(hipStreamSynchronize(st));
       ident = h[1] == 0;
       tiles_bound = ident ? S : h[0];

@@ -378,8 +378,10 @@ struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
   int ks;  // bucket = key >> ks
 };
+// before_sync (optional): run (once) just before the sort's one host wait (its last pass's
+// tile-total readback), e.g. to queue the other lane's sort first
 BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
-                            int keybits, uint32_t *valid);
+                            int bucket_bits, uint32_t *valid, std::function<void()> *before_sync = nullptr);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);

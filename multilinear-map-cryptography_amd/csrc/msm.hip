@@ -519,7 +519,8 @@ static unsigned bits_result(MsmLane &ln) {
 // the bucket order exists (or right away when there is none).
 // canon: the canonical scalars from bits_launch (n > 64).
 static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
-                            size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr) {
+                            size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr,
+                            std::function<void()> *before_sync = nullptr) {
   struct Rec {
     hipEvent_t e;
     hipStream_t s;
@@ -577,7 +578,8 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   if (!ctx->msm_cub_sort) {
     TNS_PROF_ON(ctx, st, "msm_sort", 32.0 * n + 16.0 * total);
     valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
-    const BucketOrder o = bucket_sort_dev(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid);
+    const BucketOrder o =
+        bucket_sort_dev(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid, before_sync);
     keys2 = o.keys;
     vals2 = o.vals;
     bstart = o.bstart;
@@ -784,13 +786,21 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sb, hipEventDisableTiming));
-  msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sorted ? sorted : sa);
   if (sorted) {  // staggered: lane 1 sorts under lane 0's accumulation
+    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sorted);
     TNS_HIP(hipEventRecord(sa, l0.stream));
     TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
     (void)hipEventDestroy(sorted);
+    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
+  } else {
+    // lane 1's sort is queued before lane 0's sort waits on the host for its last pass, so the
+    // two sorts' passes run side by side instead of one after the other
+    std::function<void()> sort_b = [&]() { msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb); };
+    const char *ov = getenv("TNS_SORT_OVERLAP");  // =0: lane 1's sort after lane 0's (A/B)
+    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa,
+                    ov && ov[0] == '0' ? nullptr : &sort_b);
+    if (sort_b) sort_b();
   }
-  msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
   if (!ctx->msm_stagger) {
     // both (memory-bound) sorts first, then both accumulations: an accumulation launched
     // while the other lane still sorts takes every slot and stalls that sort behind it
