@@ -266,18 +266,94 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
 
 // bucket values: empty -> identity; a run inside one chunk is already in buckets[bk];
 // a run across chunks tf < tl -> tail(tf) + heads of (tf, tl) (via the levels) + head(tl)
+// Runs over more than FIX_WAVE_SPAN chunks are summed by the whole wave that meets them in
+// k_bucket_fixup: a single thread's chain over their ~50+ items would be the tail of the whole
+// MSM (a skewed input puts every entry in one bucket: Shout's identity lookups, 5.8 instead of
+// 6.4 ms at 2^20).  Shorter runs stay one thread each -- thousands of moderately heavy buckets
+// (the top window's narrow digits crowd the low ones) are cheaper so than as thousands of
+// mostly idle wave passes next to the other lane's accumulation.
+constexpr size_t FIX_WAVE_SPAN = 512;
+
+// the items of a run across chunks tf < tl, in order: tail(tf), head(tl), then the inner heads
+// (tf, tl), peeled to FIX_FAN-aligned ranges and climbing a level whenever both ends are aligned
+struct FixItems {
+  size_t tf, tl, lo, hi;
+  int l, k;  // level, items produced so far
+  __device__ FixItems(size_t f, size_t t) : tf(f), tl(t), lo(f + 1), hi(t), l(0), k(0) {}
+  __device__ const G1Xyzz *next(const HeadTail *ht, const FixLevels &F) {
+    if (k == 0) {
+      k++;
+      return &ht[tf].tail;
+    }
+    if (k == 1) {
+      k++;
+      return &ht[tl].head;
+    }
+    for (;;) {
+      if (lo >= hi) return nullptr;
+      const bool climb = l < F.n && hi - lo >= 2 * FIX_FAN;
+      if (climb && lo % FIX_FAN == 0 && hi % FIX_FAN == 0) {
+        lo /= FIX_FAN;
+        hi /= FIX_FAN;
+        l++;
+        continue;
+      }
+      size_t i;
+      if (!climb || lo % FIX_FAN) i = lo++;
+      else i = --hi;  // lo aligned, hi not
+      k++;
+      return l == 0 ? &ht[i].head : &F.lv[l][i];
+    }
+  }
+};
+
 __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
                                                       const uint32_t *__restrict__ end,
                                                       const HeadTail *__restrict__ ht, FixLevels F,
-                                                      G1Xyzz *__restrict__ buckets, size_t nb, int acc_k) {
-  for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb;
-       bk += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t s = start[bk], e = end[bk];
+                                                      G1Xyzz *__restrict__ buckets, size_t nb, int acc_k, bool waves) {
+  const int lane = threadIdx.x & 63;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  // wave-uniform trip count: a wave meets its lanes' heavy runs together
+  for (size_t base = blockIdx.x * (size_t)blockDim.x + (threadIdx.x & ~63u); base < nb; base += stride) {
+    const size_t bk = base + lane;
+    uint32_t s = 0, e = 0;
+    if (bk < nb) {
+      s = start[bk];
+      e = end[bk];
+    }
+    const size_t tf = s / acc_k, tl = e > s ? (e - 1) / acc_k : tf;
+    const bool heavy = waves && bk < nb && tl - tf > FIX_WAVE_SPAN;
+    // the wave's heavy runs, one at a time: lane j adds items j, j + 64, ..., then a butterfly
+    for (uint64_t hm = __ballot(heavy); hm; hm &= hm - 1) {
+      const int src = __ffsll((unsigned long long)hm) - 1;
+      const size_t hf = __shfl((unsigned)tf, src), hl = __shfl((unsigned)tl, src);
+      FixItems it(hf, hl);
+      G1Xyzz acc = G1Xyzz::inf();
+      const G1Xyzz *mine = nullptr;
+      for (int k = 0;; k++) {  // the item sequence is the same in every lane: uniform control flow
+        const G1Xyzz *item = it.next(ht, F);
+        if (item && (k & 63) == lane) mine = item;
+        if (!item || (k & 63) == 63) {  // a round of 64 items: every lane adds its own at once
+          if (mine) acc = xyzz_add_lazy(acc, *mine);
+          mine = nullptr;
+          if (!item) break;
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        G1Xyzz o;
+        const uint32_t *pa = reinterpret_cast<const uint32_t *>(&acc);
+        uint32_t *po = reinterpret_cast<uint32_t *>(&o);
+#pragma unroll
+        for (int q = 0; q < (int)(sizeof(G1Xyzz) / 4); q++) po[q] = __shfl_xor(pa[q], off);
+        acc = xyzz_add_lazy(acc, o);
+      }
+      if (lane == src) buckets[bk] = acc;
+    }
+    if (bk >= nb || heavy) continue;
     if (s == e) {
       buckets[bk] = G1Xyzz::inf();
       continue;
     }
-    const size_t tf = s / acc_k, tl = (e - 1) / acc_k;
     if (tf == tl) continue;
     // one addition site: the items are head(tl), then the inner heads (tf, tl), peeled
     // to FIX_FAN-aligned ranges and climbing a level whenever both ends are aligned
@@ -673,7 +749,9 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
         TNS_LAUNCH_CHECK();
       }
     }
-    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb, acc_k);
+    const char *hv = getenv("TNS_FIX_WAVES");  // =0: every run summed by one thread (A/B)
+    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb, acc_k,
+                                                        !(hv && hv[0] == '0'));
     TNS_LAUNCH_CHECK();
   }
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
