@@ -798,15 +798,13 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   std::memcpy(out->sumcheck_challenges, chal, 32 * (size_t)nv);
   std::memcpy(out->final_evaluation, &fe, 32);
   timing[3] = t_sc.ms();
-  // challenge_field_elements("opening_challenges", nv) (src/utils.rs:195-203); only [0] used
+  // challenge_field_elements("opening_challenges", nv) (src/utils.rs:195-203); only [0] is used
+  // (src/twist.rs:219-226, src/shout.rs:189-195), and elements 1..nv-1 only extend a transcript
+  // that nothing reads afterwards, so they are not derived (no observable output depends on
+  // them; ~0.1 ms of host hashing in front of the openings at nv = 24)
   Timer t_open;
   if (nv >= 1) {
     Fr z = tr.challenge("opening_challenges_0");
-    char lab[64];
-    for (unsigned i = 1; i < nv; i++) {
-      snprintf(lab, sizeof lab, "opening_challenges_%u", i);
-      (void)tr.challenge(lab);
-    }
     std::memcpy(out->opening_point, &z, 32);
     Fr v[2];
     G1Affine pi[2];
