@@ -14,13 +14,13 @@ import json
 import sys
 
 STAGES = {
-    "msm_digits": (["k_digits", "k_scalar_bits"], 2),  # the commitments (openings arrive canonical)
+    "msm_digits": (["k_digits", "k_scalar_bits", "k_u64_tables"], 2),  # the commitments (openings arrive canonical)
     "msm_sort": (["rocprim", "k_bucket_bounds", "k_bs_"], 4),
     "msm_accumulate": (["k_accumulate"], 4),
     "msm_fixup": (["k_fix_level", "k_bucket_fixup"], 4),
     "msm_reduce": (["k_reduce_level", "k_masked_sums", "k_sum_chunks", "k_set_sum"], 4),
     "open_scan": (["k_node_chain", "k_prod_reduce", "k_node_finish", "k_sum_reduce", "k_node_quotient"], 2),
-    "sumcheck_round": (["k_sc_round", "k_sum_partials4"], None),
+    "sumcheck_round": (["k_sc_round", "k_sc_fold3", "k_sc_fold_tail", "k_sum_partials4"], None),
 }
 
 
@@ -46,8 +46,8 @@ def main():
     for st, (pats, launches) in STAGES.items():
         fk = sum(v for k, (v, _) in f.items() if any(p in k for p in pats))
         wk = sum(v for k, (v, _) in w.items() if any(p in k for p in pats))
-        if launches is None:  # sum-check: one launch per round
-            launches = max([n for k, (_, n) in f.items() if "k_sc_round" in k] or [1])
+        if launches is None:  # sum-check: its fold launches
+            launches = max(1, sum(n for k, (_, n) in f.items() if any(p in k for p in pats)))
         fb, wb = fk * 1024 * 2 / launches, wk * 1024 / launches
         res[st] = {"hbm_bytes_per_launch": fb + wb, "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                    "fetch_kib_raw_per_step": fk, "write_kib_raw_per_step": wk, "launches_per_step": launches}
