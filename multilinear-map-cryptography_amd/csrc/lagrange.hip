@@ -35,52 +35,19 @@ namespace tns {
 constexpr unsigned NODE_THREADS = 512 * 256;  // batch-inversion chains (one Fermat inverse each)
 
 // chain t: elements i = t + k*T.  pre[i] = prod of earlier (x - i') of the chain; cp[t] = chain
-// product; icp[t] = 1 / cp[t] by a batch inversion over the block (prefix and suffix products
-// across its 256 chains, one Fermat inverse per block instead of one per chain: the per-chain
-// inverses were ~30 % of k_node_finish2's multiplies).  Node `skip` (x itself, when opening at a
-// node) contributes the factor 1.  blockDim.x == 256.
+// product.  Node `skip` (x itself, when opening at a node) contributes the factor 1.
 __global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr Tm, size_t skip,
-                                                    Fr *__restrict__ pre, Fr *__restrict__ cp,
-                                                    Fr *__restrict__ icp) {
-  __shared__ Fr sh[256];
-  __shared__ Fr inv_total;
-  const int tid = threadIdx.x;
-  const size_t t = blockIdx.x * (size_t)blockDim.x + tid;
+                                                    Fr *__restrict__ pre, Fr *__restrict__ cp) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)t));  // x - i, stepping by -T
   Fr acc = Fr::one();
-  if (t < T) {
-    Fr d = sub(x, from_u64<FrCfg>((uint64_t)t));  // x - i, stepping by -T
-    for (size_t i = t; i < n; i += T) {
-      pre[i] = acc;
-      if (i != skip) acc = mul(acc, d);
-      d = sub(d, Tm);
-    }
-    cp[t] = acc;
+  for (size_t i = t; i < n; i += T) {
+    pre[i] = acc;
+    if (i != skip) acc = mul(acc, d);
+    d = sub(d, Tm);
   }
-  // inclusive prefix products lo_t = prod_{s <= t} a_s and suffix products hi_t = prod_{s >= t} a_s
-  Fr lo = acc, hi = acc;
-  for (int off = 1; off < 256; off <<= 1) {
-    sh[tid] = lo;
-    __syncthreads();
-    const Fr o = tid >= off ? sh[tid - off] : Fr::one();
-    __syncthreads();
-    lo = mul(o, lo);
-  }
-  for (int off = 1; off < 256; off <<= 1) {
-    sh[tid] = hi;
-    __syncthreads();
-    const Fr o = tid + off < 256 ? sh[tid + off] : Fr::one();
-    __syncthreads();
-    hi = mul(hi, o);
-  }
-  if (tid == 0) inv_total = inv(hi);  // hi_0 = the block's product
-  sh[tid] = lo;
-  __syncthreads();
-  const Fr before = tid ? sh[tid - 1] : Fr::one();  // prod_{s < t}
-  __syncthreads();
-  sh[tid] = hi;
-  __syncthreads();
-  const Fr after = tid < 255 ? sh[tid + 1] : Fr::one();  // prod_{s > t}
-  if (t < T) icp[t] = mul(mul(before, after), inv_total);
+  cp[t] = acc;
 }
 
 // out[blockIdx.x] = prod of in[i] over the block's grid-stride share (one level of a product tree)
@@ -117,7 +84,7 @@ static void prod_reduce(hipStream_t st, const Fr *in, size_t n, Fr *tmp, Fr *out
 template <bool BASIS>
 // (pre and out may alias: each element's pre is read before its output is written)
 __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, Fr Tm, size_t skip, Fr yoff,
-                                                     const Fr *pre, const Fr *__restrict__ icp,
+                                                     const Fr *pre, const Fr *__restrict__ cp,
                                                      const Fr *__restrict__ w, const Fr *__restrict__ y,
                                                      const Fr *__restrict__ ell, Fr *out, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -129,7 +96,7 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
   const size_t cnt = (n - 1 - t) / T;  // index of the chain's last element
   size_t i = t + cnt * T;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
-  Fr iv = icp[t];  // 1 / chain product (k_node_chain)
+  Fr iv = inv(cp[t]);
   Fr s = Fr::zero();
   const Fr L = BASIS ? ell[0] : Fr::one();
   for (;;) {
@@ -152,7 +119,7 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
 // k_node_finish<false> for two vectors on the same nodes: the inverses are shared.
 //   inv[i] = inv_i;  sp[t] = sum_chain w_i y0_i inv_i,  sp[T + t] = sum_chain w_i y1_i inv_i
 __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
-                                                      const Fr *__restrict__ icp, const Fr *__restrict__ w,
+                                                      const Fr *__restrict__ cp, const Fr *__restrict__ w,
                                                       const Fr *__restrict__ y0, const Fr *__restrict__ y1,
                                                       Fr *invs, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -164,7 +131,7 @@ __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, 
   const size_t cnt = (n - 1 - t) / T;
   size_t i = t + cnt * T;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
-  Fr iv = icp[t];  // 1 / chain product (k_node_chain)
+  Fr iv = inv(cp[t]);
   Fr s0 = Fr::zero(), s1 = Fr::zero();
   for (;;) {
     const Fr inv_i = mul(iv, pre[i]);
@@ -296,7 +263,7 @@ static size_t chain_count(size_t n) {
 struct NodeSweep {
   size_t T;
   Fr Tm;
-  Fr *cp, *icp, *sp, *dev;  // chain products and their inverses, partial sums, device scalars
+  Fr *cp, *sp, *dev;  // chain products, partial sums, device scalars
 };
 
 // chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
@@ -304,12 +271,11 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
-  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (4 * s.T + 4 + 256));
+  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (3 * s.T + 4 + 256));
   s.cp = ws;
   s.sp = ws + s.T;  // 2T: room for two vectors' partial sums
-  s.icp = ws + 3 * s.T;
-  s.dev = ws + 4 * s.T;
-  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp, s.icp);
+  s.dev = ws + 3 * s.T;
+  k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp);
   TNS_LAUNCH_CHECK();
   prod_reduce(c->stream, s.cp, s.T, s.dev + 4, s.dev);
   return s;
@@ -339,7 +305,7 @@ const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t
   const Fr xs = fr_shift(srs.tau, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, sc);
   k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
-                                                                           sc, s.icp, w, nullptr, ecp + TG, sc, nullptr);
+                                                                           sc, s.cp, w, nullptr, ecp + TG, sc, nullptr);
   TNS_LAUNCH_CHECK();
   LagrangeBasis *b = new LagrangeBasis();
   try {
@@ -361,7 +327,7 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
   const Fr xs = fr_shift(z, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
   k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
-                                                                            inv, s.icp, w, y, nullptr, inv, s.sp);
+                                                                            inv, s.cp, w, y, nullptr, inv, s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
   TNS_LAUNCH_CHECK();
@@ -383,7 +349,7 @@ void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q)
   TNS_HIP(hipStreamSynchronize(c->stream));
   const Fr xs = from_u64<FrCfg>((uint64_t)j0);
   NodeSweep s = node_sweep_begin(c, xs, N, q, j0);
-  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, N, s.T, s.Tm, j0, v, q, s.icp, w, y,
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, N, s.T, s.Tm, j0, v, q, s.cp, w, y,
                                                                             nullptr, q, s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
@@ -407,7 +373,7 @@ void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, si
   const Fr *w = bary_weights(c, N, first, cnt);
   const Fr xs = fr_shift(z, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
-  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.icp, w, y0, y1, inv,
+  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.cp, w, y0, y1, inv,
                                                                       s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
