@@ -6,6 +6,8 @@ evaluations through [L_j(tau)]G; these tests pin that path to the oracle's
 interpolate-then-commit restatement and to the device coefficient path, including its
 fallbacks (uploaded SRS without tau, tau a node, challenge z a node).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -130,7 +132,7 @@ def test_twist_proof_identical_on_both_paths(logn):
     assert a == b
 
 
-@pytest.mark.parametrize("logn", [18, 20])
+@pytest.mark.parametrize("logn", [18, 20, 24])
 def test_twist_long_barycentric_chains_match_fast_cpu(logn):
     """From 2^18 nodes the barycentric batch inversion runs 131072 chains of >= 2 nodes each (the
     smaller parity cases have one node per chain): the GPU proof equals oracle/fastcpu.c's (the
@@ -143,7 +145,8 @@ def test_twist_long_barycentric_chains_match_fast_cpu(logn):
     addr, val, isw = ts.bench_trace(1 << L, n)
     g = ts.Twist(pp).prove_soa(addr, val, isw)
     lag = pp.commitment_params.srs.lagrange_points(n)
-    st, want = co.fast_twist_prove(lag, co.bary_weights(n), pp.max_operations, addr, val, isw, 8)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))  # 2^24 (C4 itself): ~30 s on 16 threads
+    st, want = co.fast_twist_prove(lag, co.bary_weights(n), pp.max_operations, addr, val, isw, threads)
     assert st == 0
     assert g.address_commitment.commitment == want["address_commitment"]
     assert g.value_commitment.commitment == want["value_commitment"]
