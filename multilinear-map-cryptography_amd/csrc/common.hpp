@@ -351,6 +351,30 @@ __device__ __forceinline__ unsigned fr_bit_length(const Fr &k) {
     if (k.v[l]) b = 32 * l + 32 - __builtin_clz(k.v[l]);
   return b;
 }
+// max over the block of (b0, b1) -> one atomicMax per block and target (blockDim.x a multiple
+// of 64, at most 1024; every thread of the block calls it).  A per-wave atomic on one address
+// serialises in L2: 8 K of them were ~80 us of a 2^20-scalar bit-length pass.
+__device__ __forceinline__ void block_atomic_max2(unsigned b0, unsigned b1, unsigned *dst0, unsigned *dst1) {
+  __shared__ unsigned wmax[2][16];
+  for (int o = 32; o > 0; o >>= 1) {
+    b0 = max(b0, (unsigned)__shfl_xor(b0, o));
+    b1 = max(b1, (unsigned)__shfl_xor(b1, o));
+  }
+  const int w = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    wmax[0][w] = b0;
+    wmax[1][w] = b1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < (int)(blockDim.x >> 6); i++) {
+      b0 = max(b0, wmax[0][i]);
+      b1 = max(b1, wmax[1][i]);
+    }
+    if (b0) atomicMax(dst0, b0);
+    if (b1 && dst1) atomicMax(dst1, b1);
+  }
+}
 struct MsmArgs {
   const G1Affine *points;
   const Fr *scalars;

@@ -173,14 +173,7 @@ __global__ void __launch_bounds__(256) k_node_quotient2_canon(const Fr *__restri
     b0 = max(b0, fr_bit_length(c0));
     b1 = max(b1, fr_bit_length(c1));
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    b0 = max(b0, (unsigned)__shfl_xor(b0, o));
-    b1 = max(b1, (unsigned)__shfl_xor(b1, o));
-  }
-  if ((threadIdx.x & 63) == 0) {
-    if (b0) atomicMax(bits, b0);
-    if (b1) atomicMax(bits + 1, b1);
-  }
+  block_atomic_max2(b0, b1, bits, bits + 1);
 }
 
 // q_i = (v - y_i) * inv_i, in place over inv

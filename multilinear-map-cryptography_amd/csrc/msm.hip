@@ -112,11 +112,7 @@ __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scal
     canon[i] = k;
     b = max(b, fr_bit_length(k));
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned x = __shfl_xor(b, o);
-    b = x > b ? x : b;
-  }
-  if ((threadIdx.x & 63) == 0 && b) atomicMax(bits, b);
+  block_atomic_max2(b, 0u, bits, nullptr);
 }
 
 // shared = false: key = (w << (c-1)) | (|d| - 1), value = i | sign<<31
@@ -307,6 +303,19 @@ struct FixItems {
   }
 };
 
+// the sum over the wave of every lane's acc, in every lane (xor butterfly: 6 dependent additions)
+__device__ __forceinline__ G1Xyzz wave_sum_xyzz(G1Xyzz acc) {
+  for (int off = 32; off > 0; off >>= 1) {
+    G1Xyzz o;
+    const uint32_t *pa = reinterpret_cast<const uint32_t *>(&acc);
+    uint32_t *po = reinterpret_cast<uint32_t *>(&o);
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(G1Xyzz) / 4); q++) po[q] = __shfl_xor(pa[q], off);
+    acc = xyzz_add_lazy(acc, o);
+  }
+  return acc;
+}
+
 __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
                                                       const uint32_t *__restrict__ end,
                                                       const HeadTail *__restrict__ ht, FixLevels F,
@@ -339,14 +348,7 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
           if (!item) break;
         }
       }
-      for (int off = 32; off > 0; off >>= 1) {
-        G1Xyzz o;
-        const uint32_t *pa = reinterpret_cast<const uint32_t *>(&acc);
-        uint32_t *po = reinterpret_cast<uint32_t *>(&o);
-#pragma unroll
-        for (int q = 0; q < (int)(sizeof(G1Xyzz) / 4); q++) po[q] = __shfl_xor(pa[q], off);
-        acc = xyzz_add_lazy(acc, o);
-      }
+      acc = wave_sum_xyzz(acc);
       if (lane == src) buckets[bk] = acc;
     }
     if (bk >= nb || heavy) continue;
@@ -408,9 +410,12 @@ __global__ void __launch_bounds__(64) k_reduce_level(const G1Xyzz *__restrict__ 
 //   s < nbits: the groups gi with bit s set, enumerated directly (the k-th is k with a one
 //   inserted at bit s: every lane of a wave adds, no masked-off lanes);
 //   s == nbits, nbits + 1: T over the lower / upper half of the groups
+// wave_tree (nch a multiple of 64): the wave's 64 chunk sums are added in registers and only
+// parts[id / 64] is written -- the two 8-way k_sum_chunks passes after it (each a chain of 8
+// additions at low occupancy) become one 6-step butterfly
 __global__ void __launch_bounds__(64) k_masked_sums(const G1Xyzz *__restrict__ T, const G1Xyzz *__restrict__ S,
                                                     int sets, size_t g, int nbits, int CH,
-                                                    G1Xyzz *__restrict__ parts) {
+                                                    G1Xyzz *__restrict__ parts, bool wave_tree) {
   const int specs = nbits + 2;
   const size_t nch = g / (2 * (size_t)CH);
   for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)sets * specs * nch;
@@ -428,7 +433,12 @@ __global__ void __launch_bounds__(64) k_masked_sums(const G1Xyzz *__restrict__ T
       for (size_t k = ch * CH; k < ch * CH + CH; k++)
         acc = xyzz_add_lazy(acc, src[((k & ~lo_mask) << 1) | ((size_t)1 << sp) | (k & lo_mask)]);
     }
-    parts[id] = acc;
+    if (wave_tree) {  // the id range is a multiple of 64: every lane of the wave is here
+      acc = wave_sum_xyzz(acc);
+      if ((threadIdx.x & 63) == 0) parts[id >> 6] = acc;
+    } else {
+      parts[id] = acc;
+    }
   }
 }
 
@@ -778,9 +788,11 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
     const size_t nparts = (size_t)P.Wr * J.specs * nch;
     G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
     G1Xyzz *tmp = parts + nparts, *out = tmp + nparts;
-    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, J.nbits, CH, parts);
+    const char *wt = getenv("TNS_MASKED_TREE");  // =0: per-chunk parts + k_sum_chunks passes (A/B)
+    const bool tree = nch % 64 == 0 && !(wt && wt[0] == '0');
+    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, J.nbits, CH, parts, tree);
     TNS_LAUNCH_CHECK();
-    sum_sets(st, parts, P.Wr * J.specs, nch, tmp, out);
+    sum_sets(st, parts, P.Wr * J.specs, tree ? nch / 64 : nch, tmp, out);
     const size_t fin_n = (size_t)P.Wr * J.specs;
     char *h = (char *)ln.host.ensure(sizeof(G1Xyzz) * fin_n + 16);
     TNS_HIP(hipMemcpyAsync(h, out, sizeof(G1Xyzz) * fin_n, hipMemcpyDeviceToHost, st));

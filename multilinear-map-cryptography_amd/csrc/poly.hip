@@ -104,11 +104,7 @@ __global__ void __launch_bounds__(256) k_u64_tables(const uint64_t *__restrict__
     mont[i] = from_u64<FrCfg>(x);
     b = x ? max(b, 64u - (unsigned)__builtin_clzll(x)) : b;
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    unsigned y = __shfl_xor(b, o);
-    b = y > b ? y : b;
-  }
-  if ((threadIdx.x & 63) == 0 && b) atomicMax(bits, b);
+  block_atomic_max2(b, 0u, bits, nullptr);
 }
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits) {
   TNS_HIP(hipMemsetAsync(bits, 0, sizeof(unsigned), s));
