@@ -294,14 +294,16 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
 // compile-time plans of the pass-1 kernels: the fixed-base table windows (n = 2^20..2^26) and
 // the narrow trace commitments' per-window plans; anything else takes the runtime kernels
 struct Pass1Plan {
-  int c, W;
+  int tile, c, W;
   void (*count)(DigitArgs, int, int, size_t, uint32_t *);
   void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, uint32_t *, uint32_t *);
   int spt;
 };
-#define TNS_P1(C, W, SPT) {C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<BS_TILE, C, W, SPT>, SPT}
-static const Pass1Plan kPass1Plans[] = {TNS_P1(22, 12, 3), TNS_P1(20, 13, 3), TNS_P1(19, 14, 3), TNS_P1(17, 15, 3),
-                                        TNS_P1(16, 2, 16), TNS_P1(12, 2, 16)};
+#define TNS_P1(T, C, W, SPT) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT}
+static const Pass1Plan kPass1Plans[] = {TNS_P1(BS_TILE, 22, 12, 3), TNS_P1(BS_TILE, 20, 13, 3), TNS_P1(BS_TILE, 19, 14, 3),
+                                        TNS_P1(BS_TILE, 17, 15, 3), TNS_P1(BS_TILE, 16, 2, 16), TNS_P1(BS_TILE, 12, 2, 16),
+                                        // half tiles (half the LDS: twice the blocks per CU)
+                                        TNS_P1(4096, 22, 12, 2), TNS_P1(4096, 20, 13, 2)};
 #undef TNS_P1
 
 // bins of pass 1 -> segment starts; seg[nbins] = total = number of entries (also *valid)
@@ -491,40 +493,50 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const T *in, T *out, siz
 // one-tile segments fill it, and half the LDS doubles the blocks per CU -- pass 3 of a 2^24
 // opening MSM 1.02 -> 0.61 ms, profiles/r02_ab_sort_tiles.txt).
 static int pass_tile(int p) {
-  static int t[8] = {0};
-  static int nt = 0;
-  if (!nt) {
-    nt = 1;  // t[0] = 0: automatic
-    if (const char *e = getenv("TNS_BS_TILES")) {
-      int k = 0;
-      for (const char *q = e; *q && k < 8;) {
-        const int v = atoi(q);
-        t[k++] = v == 4096 ? 4096 : 8192;
-        while (*q && *q != ',') q++;
-        if (*q == ',') q++;
-      }
-      if (k) nt = k;
+  int t[8] = {0}, nt = 1;  // t[0] = 0: automatic (read per sort: tests switch it in-process)
+  if (const char *e = getenv("TNS_BS_TILES")) {
+    int k = 0;
+    for (const char *q = e; *q && k < 8;) {
+      const int v = atoi(q);
+      t[k++] = v == 4096 ? 4096 : v == 0 ? 0 : 8192;
+      while (*q && *q != ',') q++;
+      if (*q == ',') q++;
     }
+    if (k) nt = k;
   }
   return t[p < nt ? p : nt - 1];
 }
 
 // Groups the W*n digit entries of `scalars` by bucket (bucket_bits bits of bucket index;
-// per-window layout: window bits included).  Returns the key/value arrays holding the
-// result (two of the lane's four entry buffers), the bucket starts (bucket b =
-// [bstart[b], bstart[b+1]), b < 2^bucket_bits) and the shift from key to bucket;
-// *valid = number of entries (non-zero digits).
-BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
-                            int bucket_bits, uint32_t *valid, std::function<void()> *before_sync) {
+// per-window layout: window bits included).  The result (BucketOrder): the key/value arrays
+// holding it (two of the lane's four entry buffers), the bucket starts (bucket b =
+// [bstart[b], bstart[b+1]), b < 2^bucket_bits) and the shift from key to bucket; *valid =
+// number of entries (non-zero digits).
+//
+// Two phases around the sort's one host wait (the last pass's tile-total readback):
+// bucket_sort_begin queues every pass up to that readback, bucket_sort_finish waits for it and
+// queues the rest.  A pair of MSMs calls begin(a), begin(b), finish(a), finish(b), so each
+// lane's last pass starts as soon as ITS readback lands (a single host wait would hold lane a's
+// last pass behind lane b's first two passes: ~1.7 ms of an idle lane per 2^24 opening pair).
+void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+                       int bucket_bits, uint32_t *valid, BucketSortJob &J) {
   hipStream_t st = ln.stream;
   const size_t E = (size_t)W * n;
   if (E >= ((size_t)1 << 32)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one bucket sort");
   if (W > BS_TILE) throw Error(TNS_ERR_COMMITMENT, "too many MSM windows");
-  uint32_t *K[2] = {(uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * E), (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * E)};
-  uint32_t *V[2] = {(uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * E), (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * E)};
+  J = BucketSortJob();
+  J.ln = &ln;
+  J.E = E;
+  J.bucket_bits = bucket_bits;
+  uint32_t **K = J.K, **V = J.V;
+  K[0] = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * E);
+  K[1] = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * E);
+  V[0] = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * E);
+  V[1] = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * E);
   DigitArgs A{scalars, n, 0, c, W, 0, shared, stride};
   if (shared)
     while ((1 << A.wb) < W) A.wb++;
+  J.wb = A.wb;
   const int keybits = bucket_bits + A.wb;
   const int npass = std::max(1, (keybits + BS_MAXBITS - 1) / BS_MAXBITS);
   int bits[8] = {0};
@@ -554,20 +566,21 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   // pass 1: scalars -> bins of the top bits[0] key bits
   const int tile1 = W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
   const Pass1Plan *ct = nullptr;
-  if (tile1 == BS_TILE && !getenv("TNS_BS_RUNTIME_PASS1"))  // (A/B: the runtime-plan kernels)
+  if (!getenv("TNS_BS_RUNTIME_PASS1"))  // (A/B: the runtime-plan kernels)
     for (const Pass1Plan &p : kPass1Plans)
-      if (p.c == c && p.W == W) ct = &p;
+      if (p.tile == tile1 && p.c == c && p.W == W) ct = &p;
   A.spb = (size_t)tile1 / W;
   if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
   const size_t T1 = (n + A.spb - 1) / A.spb;
   int nb = 1 << bits[0];
   const size_t max_seg = (size_t)1 << keybits;
-  uint32_t *seg[2] = {(uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1)),
-                      (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1))};
+  uint32_t **seg = J.seg;
+  seg[0] = (uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1));
+  seg[1] = (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1));
   const size_t max_tiles = (E + 4095) / 4096 + (max_seg >> bits[npass - 1]) + 1;  // smallest tile: 4096
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
-  uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
-  uint32_t *offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
+  uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
+  uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
   else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
   TNS_LAUNCH_CHECK();
@@ -579,77 +592,108 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
   k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
   TNS_LAUNCH_CHECK();
 
-  size_t S = nb;
-  int cur = 0;
-  uint32_t *tcount = (uint32_t *)ln.ws[14].ensure(sizeof(uint32_t) * 2 * (max_seg + 1));
-  uint32_t *tbase = tcount + (max_seg + 1);
-  uint32_t *desc = (uint32_t *)ln.ws[15].ensure(sizeof(uint32_t) * max_tiles);
+  J.S = nb;
+  J.cur = 0;
+  J.tcount = (uint32_t *)ln.ws[14].ensure(sizeof(uint32_t) * 2 * (max_seg + 1));
+  J.tbase = J.tcount + (max_seg + 1);
+  J.desc = (uint32_t *)ln.ws[15].ensure(sizeof(uint32_t) * max_tiles);
+  J.mcount = (uint32_t *)ln.ws[17].ensure(sizeof(uint32_t) * 2 * (max_seg + 1));
+  J.mbase = J.mcount + (max_seg + 1);
+  J.npass = npass;
+  J.shift = shift;
   for (int p = 1; p < npass; p++) {
-    nb = 1 << bits[p];
-    shift -= bits[p];
+    J.nb = 1 << bits[p];
+    J.shift -= bits[p];
     int tile = pass_tile(p);
     if (!tile) tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
+    J.tile = tile;
     // In the last pass most segments fit one tile and rank locally; only segments of >= 2
     // tiles need the histogram pass and the global scan, so their counts get a compact layout,
     // sized from a readback of the tile totals (the top window's narrow digits make the
     // low-magnitude buckets' segments multi-tile).  All one-tile: no geometry at all (at 2^24
     // the full layout's histograms and scan over 512 bins x every tile took 0.34 ms).
-    int ident = 0;
-    const uint32_t *mb = nullptr;
-    size_t tiles_bound = (E + tile - 1) / tile + S, scan_len = (size_t)nb * tiles_bound + 1;
-    uint32_t *mcount = (uint32_t *)ln.ws[17].ensure(sizeof(uint32_t) * 2 * (max_seg + 1)), *mbase = mcount + (max_seg + 1);
-    const bool last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
-    k_bs_tiles<<<grid_for(S + 1, 256), 256, 0, st>>>(seg[cur], S, (uint32_t)tile, tcount, last ? mcount : nullptr);
+    J.last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
+    k_bs_tiles<<<grid_for(J.S + 1, 256), 256, 0, st>>>(seg[J.cur], J.S, (uint32_t)tile, J.tcount,
+                                                         J.last ? J.mcount : nullptr);
     TNS_LAUNCH_CHECK();
-    exclusive_scan(st, ln.ws[9], tcount, tbase, S + 1);
-    if (last) {
-      exclusive_scan(st, ln.ws[9], mcount, mbase, S + 1);
+    exclusive_scan(st, ln.ws[9], J.tcount, J.tbase, J.S + 1);
+    if (J.last) {  // the readback; pass_rest runs after bucket_sort_finish's wait
+      exclusive_scan(st, ln.ws[9], J.mcount, J.mbase, J.S + 1);
       uint32_t *h = (uint32_t *)ln.host2.ensure(2 * sizeof(uint32_t));
-      TNS_HIP(hipMemcpyAsync(h, tbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      TNS_HIP(hipMemcpyAsync(h + 1, mbase + S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      if (before_sync && *before_sync) {  // e.g. the other lane's sort, enqueued before this wait
-        auto f = std::move(*before_sync);
-        *before_sync = nullptr;
-        f();
-      }
-      TNS_HIP(hipStreamSynchronize(st));
-      ident = h[1] == 0;
-      tiles_bound = ident ? S : h[0];
-      mb = mbase;
-      scan_len = (size_t)nb * h[1] + 1;
+      TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      J.pending = true;
+      return;
     }
-    if (!ident) {
-      k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(tbase, S, desc);
-      TNS_LAUNCH_CHECK();
-    }
-    PassGeom G{seg[cur], tbase, desc, shift, nb, (uint32_t)nb - 1, ident, mb};
-    if (!ident) {
-      if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
-      if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
-      else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, K[cur], counts);
-      TNS_LAUNCH_CHECK();
-      exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
-    }
-    if (tile == 4096)
-      k_bs_scatter<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1],
-                                                                     V[cur ^ 1], seg[cur ^ 1]);
-    else
-      k_bs_scatter<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, K[cur], V[cur], K[cur ^ 1],
-                                                                        V[cur ^ 1], seg[cur ^ 1]);
-    TNS_LAUNCH_CHECK();
-    k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, seg[cur ^ 1]);
-    TNS_LAUNCH_CHECK();
-    cur ^= 1;
-    S *= nb;
+    bucket_sort_pass_rest(J, false);
   }
-  uint32_t *bstart = seg[cur];
-  if (A.wb) {  // (bucket, window) segments -> bucket starts
-    bstart = seg[cur ^ 1];
-    const size_t nbk = (size_t)1 << bucket_bits;
-    k_bs_bucket_starts<<<grid_for(nbk + 1, 256), 256, 0, st>>>(seg[cur], nbk, A.wb, bstart);
+}
+
+// the rest of pass (J.nb, J.shift, J.tile) after its tile counts: geometry, histograms, scan,
+// scatter, next segment starts.  readback: the last pass, whose tile totals are in host2.
+void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
+  MsmLane &ln = *J.ln;
+  hipStream_t st = ln.stream;
+  const int nb = J.nb, tile = J.tile, cur = J.cur;
+  const size_t S = J.S;
+  int ident = 0;
+  const uint32_t *mb = nullptr;
+  size_t tiles_bound = (J.E + tile - 1) / tile + S, scan_len = (size_t)nb * tiles_bound + 1;
+  if (readback) {
+    const uint32_t *h = (const uint32_t *)ln.host2.p;
+    ident = h[1] == 0;
+    tiles_bound = ident ? S : h[0];
+    mb = J.mbase;
+    scan_len = (size_t)nb * h[1] + 1;
+  }
+  if (!ident) {
+    k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(J.tbase, S, J.desc);
     TNS_LAUNCH_CHECK();
   }
-  return BucketOrder{K[cur], V[cur], bstart, A.wb};
+  PassGeom G{J.seg[cur], J.tbase, J.desc, J.shift, nb, (uint32_t)nb - 1, ident, mb};
+  uint32_t *counts = J.counts, *offs = J.offs;
+  if (!ident) {
+    if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
+    if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    TNS_LAUNCH_CHECK();
+    exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
+  }
+  if (tile == 4096)
+    k_bs_scatter<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, J.K[cur], J.V[cur], J.K[cur ^ 1],
+                                                                   J.V[cur ^ 1], J.seg[cur ^ 1]);
+  else
+    k_bs_scatter<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, J.K[cur], J.V[cur], J.K[cur ^ 1],
+                                                                      J.V[cur ^ 1], J.seg[cur ^ 1]);
+  TNS_LAUNCH_CHECK();
+  k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, J.seg[cur ^ 1]);
+  TNS_LAUNCH_CHECK();
+  J.cur ^= 1;
+  J.S *= nb;
+}
+
+BucketOrder bucket_sort_finish(BucketSortJob &J) {
+  MsmLane &ln = *J.ln;
+  if (J.pending) {
+    TNS_HIP(hipStreamSynchronize(ln.stream));  // the last pass's tile totals (host2)
+    J.pending = false;
+    bucket_sort_pass_rest(J, true);
+  }
+  uint32_t *bstart = J.seg[J.cur];
+  if (J.wb) {  // (bucket, window) segments -> bucket starts
+    bstart = J.seg[J.cur ^ 1];
+    const size_t nbk = (size_t)1 << J.bucket_bits;
+    k_bs_bucket_starts<<<grid_for(nbk + 1, 256), 256, 0, ln.stream>>>(J.seg[J.cur], nbk, J.wb, bstart);
+    TNS_LAUNCH_CHECK();
+  }
+  return BucketOrder{J.K[J.cur], J.V[J.cur], bstart, J.wb};
+}
+
+BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+                            int bucket_bits, uint32_t *valid) {
+  BucketSortJob J;
+  bucket_sort_begin(ln, scalars, n, c, W, shared, stride, bucket_bits, valid, J);
+  return bucket_sort_finish(J);
 }
 
 }  // namespace tns

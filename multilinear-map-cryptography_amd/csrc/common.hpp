@@ -402,10 +402,24 @@ struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
   int ks;  // bucket = key >> ks
 };
-// before_sync (optional): run (once) just before the sort's one host wait (its last pass's
-// tile-total readback), e.g. to queue the other lane's sort first
+// A sort in flight between bucket_sort_begin (every pass up to the last pass's tile-total
+// readback, queued on the lane) and bucket_sort_finish (waits for that readback, queues the rest).
+struct BucketSortJob {
+  MsmLane *ln = nullptr;
+  size_t E = 0, S = 0;
+  int bucket_bits = 0, wb = 0, npass = 0, cur = 0, nb = 0, shift = 0, tile = 0;
+  bool last = false, pending = false;
+  uint32_t *K[2] = {nullptr, nullptr}, *V[2] = {nullptr, nullptr}, *seg[2] = {nullptr, nullptr};
+  uint32_t *counts = nullptr, *offs = nullptr, *tcount = nullptr, *tbase = nullptr, *desc = nullptr;
+  uint32_t *mcount = nullptr, *mbase = nullptr;
+};
+void bucket_sort_begin(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+                       int bucket_bits, uint32_t *valid, BucketSortJob &J);
+void bucket_sort_pass_rest(BucketSortJob &J, bool readback);
+BucketOrder bucket_sort_finish(BucketSortJob &J);
+// both phases at once (single MSMs)
 BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
-                            int bucket_bits, uint32_t *valid, std::function<void()> *before_sync = nullptr);
+                            int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);

@@ -578,6 +578,9 @@ struct MsmJob {
   int L0 = 0, nbits = 0, specs = 0;
   // between the sort phase and the accumulation phase
   bool sorted = false;
+  bool sort_pending = false;        // bucket_sort_begin done, msm_finish_sort not yet
+  BucketSortJob bs;
+  hipEvent_t sorted_ev = nullptr;   // recorded on the lane once the bucket order exists
   const G1Affine *points = nullptr;
   uint32_t *keys2 = nullptr, *vals2 = nullptr, *bstart = nullptr, *bend = nullptr, *valid = nullptr;
   int ks = 0, acc_k = 0;
@@ -604,21 +607,23 @@ static unsigned bits_result(MsmLane &ln) {
 // (all scalars zero, n <= 64) finish here.  `sorted` (optional) is recorded on the lane once
 // the bucket order exists (or right away when there is none).
 // canon: the canonical scalars from bits_launch (n > 64).
+// defer: stop before the bucket sort's host wait (its last pass's readback); msm_finish_sort
+// completes it, so a pair of MSMs can queue both lanes' passes before either waits.
+static void msm_finish_sort(MsmJob &J);
 static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
                             size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr,
-                            std::function<void()> *before_sync = nullptr) {
-  struct Rec {
-    hipEvent_t e;
-    hipStream_t s;
-    ~Rec() {
-      if (e) (void)hipEventRecord(e, s);
-    }
-  } rec{sorted, ln.stream};
+                            bool defer = false) {
   J.lane = &ln;
+  J.sorted_ev = sorted;
   hipStream_t st = ln.stream;
+  auto record_now = [&]() {
+    if (J.sorted_ev) TNS_HIP(hipEventRecord(J.sorted_ev, st));
+    J.sorted_ev = nullptr;
+  };
   if (n == 0 || bits == 0) {  // all scalars zero
     J.immediate = true;
     J.result = G1Xyzz::inf();
+    record_now();
     return;
   }
   if (n <= 64) {
@@ -627,6 +632,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
     TNS_LAUNCH_CHECK();
     TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz)), d, sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
     J.tiny = true;
+    record_now();
     return;
   }
   if (n >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM larger than 2^31 points");
@@ -658,60 +664,62 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
     acc_k = 128;
     while (acc_k > 32 && total / acc_k < want) acc_k /= 2;
   }
-  const size_t nchunks = (total + acc_k - 1) / acc_k;
-  uint32_t *keys2, *vals2, *bstart, *bend, *valid;
-  int ks = 0;  // bucket = key >> ks
+  J.points = points;
+  J.acc_k = acc_k;
+  J.nchunks = (total + acc_k - 1) / acc_k;
+  J.n = n;
   if (!ctx->msm_cub_sort) {
     TNS_PROF_ON(ctx, st, "msm_sort", 32.0 * n + 16.0 * total);
-    valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
-    const BucketOrder o =
-        bucket_sort_dev(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, valid, before_sync);
-    keys2 = o.keys;
-    vals2 = o.vals;
-    bstart = o.bstart;
-    bend = o.bstart + 1;
-    ks = o.ks;
-  } else {
-    uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
-    uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
-    keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
-    vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
-    uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
-    bstart = bounds;
-    bend = bounds + P.nb;
-    valid = bounds + 2 * P.nb;
-    {
-      TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
-      k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
-                                                 keys, vals);
-      TNS_LAUNCH_CHECK();
-    }
-    size_t temp_bytes = 0;
-    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
-                                               P.end_bit, st));
-    void *temp = ln.ws[9].ensure(temp_bytes);
-    TNS_PROF_ON(ctx, st, "msm_sort", 16.0 * total);
-    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys2, vals, vals2, (int)total, 0,
-                                               P.end_bit, st));
-    TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
-    k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(keys2, total, P.sentinel, bstart, bend, valid);
+    J.valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
+    bucket_sort_begin(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
+    J.sort_pending = true;
+    if (!defer) msm_finish_sort(J);
+    return;
+  }
+  uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
+  uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
+  J.keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
+  J.vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
+  uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
+  J.bstart = bounds;
+  J.bend = bounds + P.nb;
+  J.valid = bounds + 2 * P.nb;
+  J.ks = 0;
+  {
+    TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
+    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
+                                               keys, vals);
     TNS_LAUNCH_CHECK();
   }
-  if (rec.e) {
-    TNS_HIP(hipEventRecord(rec.e, st));
-    rec.e = nullptr;
+  size_t temp_bytes = 0;
+  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, J.keys2, vals, J.vals2, (int)total, 0,
+                                             P.end_bit, st));
+  void *temp = ln.ws[9].ensure(temp_bytes);
+  {
+    TNS_PROF_ON(ctx, st, "msm_sort", 16.0 * total);
+    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, J.keys2, vals, J.vals2, (int)total, 0,
+                                               P.end_bit, st));
   }
+  TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
+  k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(J.keys2, total, P.sentinel, J.bstart, J.bend, J.valid);
+  TNS_LAUNCH_CHECK();
   J.sorted = true;
-  J.points = points;
-  J.keys2 = keys2;
-  J.vals2 = vals2;
-  J.bstart = bstart;
-  J.bend = bend;
-  J.valid = valid;
-  J.ks = ks;
-  J.acc_k = acc_k;
-  J.nchunks = nchunks;
-  J.n = n;
+  record_now();
+}
+
+// the bucket sort's second phase (waits for its last-pass readback), then the sorted state
+static void msm_finish_sort(MsmJob &J) {
+  if (!J.sort_pending) return;
+  J.sort_pending = false;
+  const BucketOrder o = bucket_sort_finish(J.bs);
+  J.keys2 = o.keys;
+  J.vals2 = o.vals;
+  J.bstart = o.bstart;
+  J.bend = o.bstart + 1;
+  J.ks = o.ks;
+  J.sorted = true;
+  if (J.sorted_ev) TNS_HIP(hipEventRecord(J.sorted_ev, J.lane->stream));
+  J.sorted_ev = nullptr;
 }
 
 // Phase 2 (asynchronous): accumulation, bucket fixup, reduction and the per-set sums' readback.
@@ -883,13 +891,17 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     (void)hipEventDestroy(sorted);
     msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
   } else {
-    // lane 1's sort is queued before lane 0's sort waits on the host for its last pass, so the
-    // two sorts' passes run side by side instead of one after the other
-    std::function<void()> sort_b = [&]() { msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb); };
-    const char *ov = getenv("TNS_SORT_OVERLAP");  // =0: lane 1's sort after lane 0's (A/B)
-    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa,
-                    ov && ov[0] == '0' ? nullptr : &sort_b);
-    if (sort_b) sort_b();
+    // both lanes' passes are queued before either lane's host wait (the last pass's readback),
+    // and each lane's last pass follows its own readback: the two sorts run side by side and
+    // neither waits for the other's first passes (TNS_SORT_OVERLAP=0: lane 1's sort is queued
+    // only after lane 0's sort completes, for A/B)
+    const char *ov = getenv("TNS_SORT_OVERLAP");
+    const bool overlap = !(ov && ov[0] == '0');
+    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa, overlap);
+    if (!overlap) msm_finish_sort(ja);
+    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, overlap);
+    msm_finish_sort(ja);
+    msm_finish_sort(jb);
   }
   if (!ctx->msm_stagger) {
     // both (memory-bound) sorts first, then both accumulations: an accumulation launched

@@ -162,7 +162,8 @@ def test_msm_window_tables_equal_per_window_layout(logn):
         assert a == b
 
 
-@pytest.mark.parametrize("variant", ["TNS_BS_RUNTIME_PASS1", "TNS_BS_NO_LOCAL_LAST", "TNS_MSM_W1", "TNS_FIX_WAVES"])
+@pytest.mark.parametrize("variant", ["TNS_BS_RUNTIME_PASS1", "TNS_BS_NO_LOCAL_LAST", "TNS_MSM_W1", "TNS_FIX_WAVES",
+                                     "TNS_BS_TILES", "TNS_MASKED_TREE"])
 @pytest.mark.parametrize("pattern", ["full", "addr21", "addr22", "val30", "equal"])
 def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     """The bucket sort's fast paths == its general kernels: the compile-time-plan pass 1 (c = 20,
@@ -170,7 +171,9 @@ def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     the runtime-plan kernels, the all-one-tile last pass vs the tiled one, the single
     22-bit window of 21-bit scalars vs two windows (TNS_MSM_W1=0), and runs over many chunks
     summed by one wave each vs one thread each (TNS_FIX_WAVES=0; "equal": one run per window
-    spans every chunk)."""
+    spans every chunk), half-size pass-1 tiles (TNS_BS_TILES=4096,...: the compile-time plan's
+    4096-entry variant for the table windows) and the masked sums' per-chunk parts vs their
+    wave butterfly (TNS_MASKED_TREE=0)."""
     pp, _ = params(18)
     n = 1 << 20
     rng = np.random.default_rng(len(pattern))
@@ -182,7 +185,8 @@ def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
         bits = int(pattern[-2:])
         c = ts.fr_from_u64_array(rng.integers(0, 1 << bits, size=n, dtype=np.uint64))
     a = ts.msm(pp.commitment_params, c)
-    monkeypatch.setenv(variant, "0" if variant in ("TNS_MSM_W1", "TNS_FIX_WAVES") else "1")
+    value = {"TNS_MSM_W1": "0", "TNS_FIX_WAVES": "0", "TNS_MASKED_TREE": "0", "TNS_BS_TILES": "4096,8192,4096"}
+    monkeypatch.setenv(variant, value.get(variant, "1"))
     b = ts.msm(pp.commitment_params, c)
     assert a == b
 
