@@ -15,8 +15,10 @@ Both are weak scaling: 2^24 operations per GPU.
 
 Extra fields (rank 0, N = 1): C2 MSM pairs/s at 2^20 (setup_params(18), Fr::rand scalars
 from ChaCha20Rng([7;32])), C3 Shout lookups/s (2^20-entry table, 2^20 lookups), the per-
-stage device-time breakdown, the roofline of the dominant kernel (HIP events on the
-library's stream; algorithmic bytes from SURVEY.md 8(d)), and two CPU baselines on a
+stage device-time breakdown (every stage timed by HIP events on 2 untimed steps after the
+timed region), the roofline of the dominant kernel (HIP events around its launches, on the
+lane stream it runs on, inside the timed steps -- the only events there; algorithmic bytes
+from SURVEY.md 8(d)), and two CPU baselines on a
 bounded sample (oracle/fastcpu.c with the GPU path's algorithms, and the C oracle restating
 the reference algorithms).
 """
@@ -71,6 +73,11 @@ def parse():
                     help="testing aid: every rank on device 0 with a gloo process group (one-GPU box)")
     ap.add_argument("--no-msm-tables", action="store_true",
                     help="per-window MSM buckets instead of the fixed-base window tables")
+    ap.add_argument("--stage-steps", type=int, default=2,
+                    help="untimed steps after the timed region that time every stage (stages_ms_per_step); "
+                         "the timed steps time only the roofline kernel (two HIP events per launch)")
+    ap.add_argument("--profile-all-timed", action="store_true",
+                    help="A/B: time every stage inside the timed steps (the pre-round-2 behaviour)")
     return ap.parse_args()
 
 
@@ -113,12 +120,20 @@ def max_over_ranks(pg, local, x):
     return float(t.item())
 
 
-def roofline_from_profile(ts, ctx):
+ROOF_KERNEL = "msm_accumulate"  # the dominant stage by device time (every stage timed: stages_ms_per_step)
+
+
+def read_stages(ts, ctx):
     stages = {}
     for s in ts.PROFILE_STAGES:
         ms, n, b = ts.profile_read(ctx, s)
         if n:
             stages[s] = {"ms": ms, "launches": n, "alg_bytes": b}
+    return stages
+
+
+def roofline_from_profile(ts, ctx):
+    stages = read_stages(ts, ctx)
     if not stages:
         return None, stages
     dom = max(stages, key=lambda k: stages[k]["ms"])
@@ -269,6 +284,7 @@ def main():
         prove()
     barrier_sync(pg, local)
     ts.profile_enable(ctx, True)
+    ts.profile_only(ctx, None if args.profile_all_timed else ROOF_KERNEL)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         prove()
@@ -276,6 +292,16 @@ def main():
     dt = time.perf_counter() - t0
     breakdown = ctx.timing()
     roof, stages = roofline_from_profile(ts, ctx)
+    stage_steps = args.steps
+    if not args.profile_all_timed and args.stage_steps > 0:  # every stage, on untimed steps
+        ts.profile_enable(ctx, True)
+        ts.profile_only(ctx, None)
+        for _ in range(args.stage_steps):
+            prove()
+        barrier_sync(pg, local)
+        stages = read_stages(ts, ctx)
+        stage_steps = args.stage_steps
+    ts.profile_only(ctx, None)
     ts.profile_enable(ctx, False)
     dt_max = max_over_ranks(pg, local, dt)
     total_ops = (n_total if sharded else world * n_ops) * args.steps
@@ -331,7 +357,9 @@ def main():
         out["twist_ops_per_sec_pcie_inclusive"] = round(n_ops / (time.perf_counter() - t3), 2)
     if roof is not None:
         out["roofline"] = roof
-        out["stages_ms_per_step"] = {k: round(v["ms"] / args.steps, 3) for k, v in stages.items()}
+        out["stages_ms_per_step"] = {k: round(v["ms"] / stage_steps, 3) for k, v in stages.items()}
+        out["stages_timed_on"] = ("the timed steps" if args.profile_all_timed or args.stage_steps <= 0
+                                  else f"{stage_steps} untimed steps after the timed region")
     if rank == 0 and world == 1 and not args.no_extras:
         out["cpu_baseline"] = cpu_baseline(ts, pp18, args.cpu_fast_log_ops)
         out["cpu_reference_algorithms"] = cpu_reference_algorithms(args.cpu_baseline_ops)

@@ -310,6 +310,9 @@ int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *
  * "msm_sort", "msm_digits", "msm_reduce", "ntt_stage", "ntt_lds", "ntt_pointwise",
  * "interp_tile", "sumcheck_round", "open_scan").  Enabling resets the totals. */
 int tns_profile_enable(tns_ctx *ctx, int on);
+/* Restrict the timing to one stage (NULL or "": every stage).  Each timed stage costs two HIP
+ * events per launch; the bench times only its roofline kernel inside the timed steps. */
+int tns_profile_only(tns_ctx *ctx, const char *stage);
 int tns_profile_read(tns_ctx *ctx, const char *stage, double *total_ms, uint64_t *launches,
                      double *algorithmic_bytes);
 /* out = {summed launch ms, launches, algorithmic bytes, operations (msm_accumulate: mixed

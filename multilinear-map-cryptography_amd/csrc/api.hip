@@ -1439,6 +1439,14 @@ int tns_profile_enable(tns_ctx *ctx, int on) {
   return TNS_OK;
 }
 
+int tns_profile_only(tns_ctx *ctx, const char *stage) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.prof.only = stage ? stage : "";
+    return TNS_OK;
+  });
+}
+
 int tns_profile_read_ex(tns_ctx *ctx, const char *stage, double out[5]) {
   return guarded([&]() {
     CtxScope g(&ctx->c);

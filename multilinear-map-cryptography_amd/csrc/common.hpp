@@ -167,6 +167,7 @@ struct KernelProfiler {
   };
   std::vector<Rec> pending;
   std::map<std::string, Tot> totals;
+  std::string only;  // non-empty: time this stage alone
   void start(hipStream_t s) {
     reset();
     if (!ref) (void)hipEventCreate(&ref);
@@ -219,7 +220,7 @@ struct ProfScope {
   hipStream_t s;
   KernelProfiler::Rec r;
   ProfScope(KernelProfiler &prof, hipStream_t st, const char *name, double alg_bytes) : s(st) {
-    if (!prof.enabled) return;
+    if (!prof.enabled || (!prof.only.empty() && prof.only != name)) return;
     p = &prof;
     r.name = name;
     r.bytes = alg_bytes;

@@ -1169,6 +1169,11 @@ def profile_enable(ctx: Context, on: bool = True):
     N.load().tns_profile_enable(ctx.handle, 1 if on else 0)
 
 
+def profile_only(ctx: Context, stage=None):
+    """Time only `stage` (None: every stage) while profiling is enabled."""
+    _check(N.load().tns_profile_only(ctx.handle, stage.encode() if stage else None))
+
+
 PROFILE_STAGES = ["msm_digits", "msm_sort", "msm_accumulate", "msm_fixup", "msm_reduce", "ntt_stage", "ntt_lds",
                   "ntt_pointwise", "interp_tile", "interp_elementwise", "sumcheck_round", "open_scan"]
 
