@@ -191,8 +191,6 @@ struct HeadTail {
 __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals,
                                                     const uint32_t *__restrict__ valid_p,
-                                                    const uint32_t *__restrict__ start,
-                                                    const uint32_t *__restrict__ end,
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
                                                     HeadTail *__restrict__ ht, size_t nchunks, int ks,
@@ -204,16 +202,22 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
     if (a >= valid) continue;
     const size_t b = a + acc_k < valid ? a + acc_k : valid;
     uint32_t cur = keys[a] >> ks;
+    // a run is a head (it began before this chunk) iff it is the chunk's first run and entry
+    // a - 1 has its bucket, a tail (it goes on after the chunk) iff it is the last run and entry
+    // b has its bucket: two key loads per chunk instead of the run's bounds at every flush.
+    // Flushed sums stay in the lazy domain [0, 2M): the fixup and the reduction add them lazily.
+    const bool head_run = a > 0 && (keys[a - 1] >> ks) == cur;
+    const uint32_t after = b < valid ? keys[b] >> ks : 0xffffffffu;
+    bool first = true;
     G1Xyzz acc = G1Xyzz::inf();
     for (size_t p = a;; p++) {
       const uint32_t k = (p < b) ? keys[p] >> ks : 0xffffffffu;
       if (k != cur) {  // flush the run of bucket `cur`
-        const uint32_t s = start[cur], e = end[cur];
-        acc = xyzz_canon(acc);
-        if (s < a) ht[t].head = acc;
-        else if (e > b) ht[t].tail = acc;
+        if (first && head_run) ht[t].head = acc;
+        else if (p >= b && after == cur) ht[t].tail = acc;
         else buckets[cur] = acc;
         if (p >= b) break;
+        first = false;
         cur = k;
         acc = G1Xyzz::inf();
       }
@@ -741,8 +745,8 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
   {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
-    k_accumulate<<<grid_for(nchunks, 256, acc_cap), 256, 0, st>>>(keys2, vals2, valid, bstart, bend,
-                                                                   points, buckets, ht, nchunks, ks, acc_k);
+    k_accumulate<<<grid_for(nchunks, 256, acc_cap), 256, 0, st>>>(keys2, vals2, valid, points, buckets, ht,
+                                                                   nchunks, ks, acc_k);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
