@@ -50,6 +50,44 @@ __global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr
   cp[t] = acc;
 }
 
+// icp[t] = 1 / cp[t] for t < T by one batch inversion per block of 256 chains (prefix and suffix
+// products in LDS, one Fermat inverse per block instead of one per chain: those were about a
+// third of k_node_finish2's multiplies).  A zero chain product gets 0 and leaves its block's
+// other inverses intact.  blockDim.x == 256.
+__global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, size_t T, Fr *__restrict__ icp) {
+  __shared__ Fr sh[256];
+  __shared__ Fr inv_total;
+  const int tid = threadIdx.x;
+  const size_t t = blockIdx.x * (size_t)blockDim.x + tid;
+  Fr a = t < T ? cp[t] : Fr::one();
+  const bool zero = a.is_zero();
+  if (zero) a = Fr::one();
+  Fr lo = a, hi = a;  // inclusive prefix / suffix products over the block
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = lo;
+    __syncthreads();
+    const Fr o = tid >= off ? sh[tid - off] : Fr::one();
+    __syncthreads();
+    lo = mul(o, lo);
+  }
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = hi;
+    __syncthreads();
+    const Fr o = tid + off < 256 ? sh[tid + off] : Fr::one();
+    __syncthreads();
+    hi = mul(hi, o);
+  }
+  if (tid == 0) inv_total = inv(hi);  // hi of thread 0 = the block's product
+  sh[tid] = lo;
+  __syncthreads();
+  const Fr before = tid ? sh[tid - 1] : Fr::one();  // prod over s < t
+  __syncthreads();
+  sh[tid] = hi;
+  __syncthreads();
+  const Fr after = tid < 255 ? sh[tid + 1] : Fr::one();  // prod over s > t
+  if (t < T) icp[t] = zero ? Fr::zero() : mul(mul(before, after), inv_total);
+}
+
 // out[blockIdx.x] = prod of in[i] over the block's grid-stride share (one level of a product tree)
 __global__ void __launch_bounds__(256) k_prod_reduce(const Fr *__restrict__ in, size_t n, Fr *__restrict__ out) {
   __shared__ Fr lds[256];
@@ -84,7 +122,7 @@ static void prod_reduce(hipStream_t st, const Fr *in, size_t n, Fr *tmp, Fr *out
 template <bool BASIS>
 // (pre and out may alias: each element's pre is read before its output is written)
 __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, Fr Tm, size_t skip, Fr yoff,
-                                                     const Fr *pre, const Fr *__restrict__ cp,
+                                                     const Fr *pre, const Fr *__restrict__ cp, bool inverted,
                                                      const Fr *__restrict__ w, const Fr *__restrict__ y,
                                                      const Fr *__restrict__ ell, Fr *out, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -96,7 +134,7 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
   const size_t cnt = (n - 1 - t) / T;  // index of the chain's last element
   size_t i = t + cnt * T;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
-  Fr iv = inv(cp[t]);
+  Fr iv = inverted ? cp[t] : inv(cp[t]);  // cp: the chain inverses (k_chain_inv) or products
   Fr s = Fr::zero();
   const Fr L = BASIS ? ell[0] : Fr::one();
   for (;;) {
@@ -119,7 +157,7 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
 // k_node_finish<false> for two vectors on the same nodes: the inverses are shared.
 //   inv[i] = inv_i;  sp[t] = sum_chain w_i y0_i inv_i,  sp[T + t] = sum_chain w_i y1_i inv_i
 __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
-                                                      const Fr *__restrict__ cp, const Fr *__restrict__ w,
+                                                      const Fr *__restrict__ cp, bool inverted, const Fr *__restrict__ w,
                                                       const Fr *__restrict__ y0, const Fr *__restrict__ y1,
                                                       Fr *invs, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -131,7 +169,7 @@ __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, 
   const size_t cnt = (n - 1 - t) / T;
   size_t i = t + cnt * T;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
-  Fr iv = inv(cp[t]);
+  Fr iv = inverted ? cp[t] : inv(cp[t]);  // cp: the chain inverses (k_chain_inv) or products
   Fr s0 = Fr::zero(), s1 = Fr::zero();
   for (;;) {
     const Fr inv_i = mul(iv, pre[i]);
@@ -257,6 +295,8 @@ struct NodeSweep {
   size_t T;
   Fr Tm;
   Fr *cp, *sp, *dev;  // chain products, partial sums, device scalars
+  Fr *icp;            // what the finish kernels read: the chain inverses, or cp (inverted = false)
+  bool inverted;
 };
 
 // chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
@@ -264,13 +304,21 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
-  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (3 * s.T + 4 + 256));
+  Fr *ws = (Fr *)c->scratch[5].ensure(sizeof(Fr) * (4 * s.T + 4 + 256));
   s.cp = ws;
   s.sp = ws + s.T;  // 2T: room for two vectors' partial sums
   s.dev = ws + 3 * s.T;
   k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp);
   TNS_LAUNCH_CHECK();
   prod_reduce(c->stream, s.cp, s.T, s.dev + 4, s.dev);
+  const char *ci = getenv("TNS_CHAIN_INV");  // =0: one Fermat inverse per chain in the finish kernels (A/B, tests)
+  s.inverted = !(ci && ci[0] == '0');
+  s.icp = s.cp;
+  if (s.inverted) {
+    s.icp = s.dev + 4 + 256;
+    k_chain_inv<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(s.cp, s.T, s.icp);
+    TNS_LAUNCH_CHECK();
+  }
   return s;
 }
 
@@ -298,7 +346,8 @@ const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t
   const Fr xs = fr_shift(srs.tau, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, sc);
   k_node_finish<true><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
-                                                                           sc, s.cp, w, nullptr, ecp + TG, sc, nullptr);
+                                                                           sc, s.icp, s.inverted, w, nullptr, ecp + TG, sc,
+                                                                           nullptr);
   TNS_LAUNCH_CHECK();
   LagrangeBasis *b = new LagrangeBasis();
   try {
@@ -320,7 +369,8 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
   const Fr xs = fr_shift(z, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
   k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, SIZE_MAX, Fr::zero(),
-                                                                            inv, s.cp, w, y, nullptr, inv, s.sp);
+                                                                            inv, s.icp, s.inverted, w, y, nullptr, inv,
+                                                                            s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
   TNS_LAUNCH_CHECK();
@@ -342,7 +392,8 @@ void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q)
   TNS_HIP(hipStreamSynchronize(c->stream));
   const Fr xs = from_u64<FrCfg>((uint64_t)j0);
   NodeSweep s = node_sweep_begin(c, xs, N, q, j0);
-  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, N, s.T, s.Tm, j0, v, q, s.cp, w, y,
+  k_node_finish<false><<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, N, s.T, s.Tm, j0, v, q, s.icp,
+                                                                            s.inverted, w, y,
                                                                             nullptr, q, s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
@@ -366,7 +417,8 @@ void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, si
   const Fr *w = bary_weights(c, N, first, cnt);
   const Fr xs = fr_shift(z, first);
   NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
-  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.cp, w, y0, y1, inv,
+  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.icp, s.inverted, w, y0,
+                                                                      y1, inv,
                                                                       s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);

@@ -159,6 +159,24 @@ def test_twist_long_barycentric_chains_match_fast_cpu(logn):
         assert g.address_commitment.commitment == po.affine_mul(po.G1_GEN, f_tau)
 
 
+def test_chain_inverse_batch_matches_fermat(monkeypatch):
+    """k_chain_inv (one batch inversion per block of 256 chains) == one Fermat inverse per chain
+    (TNS_CHAIN_INV=0) on the opening paths with chains of several nodes: Twist at 2^18 (the
+    two-vector k_node_finish2) and Shout with T != M (two single-vector openings)."""
+    pp, _ = params(17)  # SRS 2^19 + 1 points
+    n = 1 << 18
+    pp.commitment_params.srs.prepare_lagrange(n)
+    addr, val, isw = ts.bench_trace(1 << 16, n)
+    T, M = 1 << 18, 3 << 16
+    rng = np.random.default_rng(5)
+    entries = ts.to_mont(rand_vals(T, seed=11))
+    idx = rng.integers(0, T, size=M, dtype=np.uint64)
+    a = (ts.Twist(pp).prove_soa(addr, val, isw), ts.Shout(pp).prove_arrays(entries, idx))
+    monkeypatch.setenv("TNS_CHAIN_INV", "0")
+    b = (ts.Twist(pp).prove_soa(addr, val, isw), ts.Shout(pp).prove_arrays(entries, idx))
+    assert a == b
+
+
 @pytest.mark.parametrize("T,M", [(5, 3), (64, 1000), (4096, 17)])
 def test_shout_proof_identical_on_both_paths(T, M):
     pp, _ = params(10)  # SRS 4097 points
