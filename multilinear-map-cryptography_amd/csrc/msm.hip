@@ -728,28 +728,36 @@ static void msm_finish_sort(MsmJob &J) {
 
 // Phase 2 (asynchronous): accumulation, bucket fixup, reduction and the per-set sums' readback.
 // `accumulated` (optional) is recorded on the lane right after the accumulation kernel.
-static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = nullptr) {
+static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
   if (!J.sorted) {  // immediate / tiny: done in phase 1
     if (accumulated) TNS_HIP(hipEventRecord(accumulated, J.lane->stream));
     return;
   }
   MsmLane &ln = *J.lane;
   hipStream_t st = ln.stream;
-  const MsmPlan &P = J.P;
-  const G1Affine *points = J.points;
-  uint32_t *keys2 = J.keys2, *vals2 = J.vals2, *bstart = J.bstart, *bend = J.bend, *valid = J.valid;
-  const int ks = J.ks, acc_k = J.acc_k;
-  const size_t nchunks = J.nchunks, n = J.n;
-  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * P.nb);
-  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * nchunks);
+  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * J.P.nb);
+  HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * J.nchunks);
   {
-    TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * n);  // 96 B per (scalar, point) pair
+    TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * J.n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
-    k_accumulate<<<grid_for(nchunks, 256, acc_cap), 256, 0, st>>>(keys2, vals2, valid, points, buckets, ht,
-                                                                   nchunks, ks, acc_k);
+    k_accumulate<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets,
+                                                                     ht, J.nchunks, J.ks, J.acc_k);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
+}
+
+// the accumulation's tail: bucket fixup, reduction and the per-set sums' readback
+static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
+  if (!J.sorted) return;
+  MsmLane &ln = *J.lane;
+  hipStream_t st = ln.stream;
+  const MsmPlan &P = J.P;
+  uint32_t *keys2 = J.keys2, *bstart = J.bstart, *bend = J.bend, *valid = J.valid;
+  const int ks = J.ks, acc_k = J.acc_k;
+  const size_t nchunks = J.nchunks;
+  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].p;
+  HeadTail *ht = (HeadTail *)ln.ws[6].p;
   {
     TNS_PROF_ON(ctx, st, "msm_fixup", 0.0);
     FixLevels F{};
@@ -811,6 +819,11 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
     // the number of sorted non-zero digits = mixed additions of k_accumulate (profiling)
     TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   }
+}
+
+static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = nullptr) {
+  msm_launch_accumulate(ctx, J, accumulated);
+  msm_launch_tail(ctx, J);
 }
 
 
@@ -915,18 +928,39 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   }
   (void)hipEventDestroy(sa);
   (void)hipEventDestroy(sb);
-  if (ctx->msm_serial) {
-    // the accumulations one after the other: each is VALU-bound on the whole chip, so run
-    // together they take as long, and each launch's own duration is then its kernel time
+  // TNS_TAILS_LAST: 0 never, 1 always (A/B); default: for a pair of table-window MSMs (the
+  // openings: full-width scalars, ~17 ms accumulations whose tails are ~1.2 ms each)
+  const char *tl = getenv("TNS_TAILS_LAST");
+  const bool tails_last = tl ? tl[0] == '1' : (ja.sorted && jb.sorted && ja.P.shared && jb.P.shared);
+  if (ctx->msm_serial && tails_last) {
+    // the accumulations one after the other (each is VALU-bound on the whole chip: run together
+    // they take as long, and each launch's own duration is then its kernel time), and lane 0's
+    // fixup/reduction waits for lane 1's accumulation: under it, that tail's kernels took wave
+    // slots from the second accumulation; after it the two tails (short chains, few waves each)
+    // run side by side.  (The commitments keep lane 0's tail under lane 1's accumulation: the
+    // 22-bit address MSM's 2^22-bucket reduction is longer than the value accumulation.)
+    hipEvent_t acc_a, acc_b;
+    TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+    TNS_HIP(hipEventCreateWithFlags(&acc_b, hipEventDisableTiming));
+    msm_launch_accumulate(ctx, ja, acc_a);
+    TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
+    msm_launch_accumulate(ctx, jb, acc_b);
+    TNS_HIP(hipStreamWaitEvent(l0.stream, acc_b, 0));
+    (void)hipEventDestroy(acc_a);
+    (void)hipEventDestroy(acc_b);
+    msm_launch_tail(ctx, ja);
+    msm_launch_tail(ctx, jb);
+  } else if (ctx->msm_serial) {
     hipEvent_t acc_a;
     TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
     msm_launch_reduce(ctx, ja, acc_a);
     TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
     (void)hipEventDestroy(acc_a);
+    msm_launch_reduce(ctx, jb);
   } else {
     msm_launch_reduce(ctx, ja);
+    msm_launch_reduce(ctx, jb);
   }
-  msm_launch_reduce(ctx, jb);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
 }
