@@ -513,11 +513,13 @@ static int pass_tile(int p) {
 // [bstart[b], bstart[b+1]), b < 2^bucket_bits) and the shift from key to bucket; *valid =
 // number of entries (non-zero digits).
 //
-// Two phases around the sort's one host wait (the last pass's tile-total readback):
-// bucket_sort_begin queues every pass up to that readback, bucket_sort_finish waits for it and
-// queues the rest.  A pair of MSMs calls begin(a), begin(b), finish(a), finish(b), so each
-// lane's last pass starts as soon as ITS readback lands (a single host wait would hold lane a's
-// last pass behind lane b's first two passes: ~1.7 ms of an idle lane per 2^24 opening pair).
+// Three stages around the sort's one host wait (the last pass's tile-total readback):
+// bucket_sort_begin queues pass 1, bucket_sort_passes the passes up to that readback, and
+// bucket_sort_finish waits for it and queues the rest.  A pair of MSMs calls begin(a), begin(b),
+// passes(a), passes(b), finish(a), finish(b): lane b's pass 1 is queued after ~5 host calls
+// instead of lane a's ~20 (0.35 ms of launch overhead on the critical lane), and each lane's
+// last pass starts as soon as ITS readback lands (a single host wait would hold lane a's last
+// pass behind lane b's first two passes: ~1.7 ms of an idle lane per 2^24 opening pair).
 void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J) {
   hipStream_t st = ln.stream;
@@ -539,7 +541,7 @@ void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, b
   J.wb = A.wb;
   const int keybits = bucket_bits + A.wb;
   const int npass = std::max(1, (keybits + BS_MAXBITS - 1) / BS_MAXBITS);
-  int bits[8] = {0};
+  int *bits = J.bits;
   // the last pass sorts LDS-sized segments by BS_MAXBITS bits; the passes before it split the
   // remaining bits evenly (25-bit keys: 8, 8, 9 -- pass 2 with 256 instead of 512 bins writes
   // 128-byte runs: 1.21 -> 1.02 ms at 2^24)
@@ -601,6 +603,16 @@ void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, b
   J.mbase = J.mcount + (max_seg + 1);
   J.npass = npass;
   J.shift = shift;
+  J.keybits = keybits;
+}
+
+// passes 2 .. up to the last pass's readback (queued on the lane; no host wait)
+void bucket_sort_passes(BucketSortJob &J) {
+  MsmLane &ln = *J.ln;
+  hipStream_t st = ln.stream;
+  const int npass = J.npass, keybits = J.keybits, *bits = J.bits;
+  const size_t E = J.E;
+  uint32_t **seg = J.seg;
   for (int p = 1; p < npass; p++) {
     J.nb = 1 << bits[p];
     J.shift -= bits[p];
@@ -693,6 +705,7 @@ BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int
                             int bucket_bits, uint32_t *valid) {
   BucketSortJob J;
   bucket_sort_begin(ln, scalars, n, c, W, shared, stride, bucket_bits, valid, J);
+  bucket_sort_passes(J);
   return bucket_sort_finish(J);
 }
 

@@ -403,12 +403,14 @@ struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
   int ks;  // bucket = key >> ks
 };
-// A sort in flight between bucket_sort_begin (every pass up to the last pass's tile-total
-// readback, queued on the lane) and bucket_sort_finish (waits for that readback, queues the rest).
+// A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
+// pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
+// all but the wait are queued on the lane without blocking the host.
 struct BucketSortJob {
   MsmLane *ln = nullptr;
   size_t E = 0, S = 0;
-  int bucket_bits = 0, wb = 0, npass = 0, cur = 0, nb = 0, shift = 0, tile = 0;
+  int bucket_bits = 0, wb = 0, npass = 0, cur = 0, nb = 0, shift = 0, tile = 0, keybits = 0;
+  int bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key bits per pass
   bool last = false, pending = false;
   uint32_t *K[2] = {nullptr, nullptr}, *V[2] = {nullptr, nullptr}, *seg[2] = {nullptr, nullptr};
   uint32_t *counts = nullptr, *offs = nullptr, *tcount = nullptr, *tbase = nullptr, *desc = nullptr;
@@ -416,6 +418,7 @@ struct BucketSortJob {
 };
 void bucket_sort_begin(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J);
+void bucket_sort_passes(BucketSortJob &J);
 void bucket_sort_pass_rest(BucketSortJob &J, bool readback);
 BucketOrder bucket_sort_finish(BucketSortJob &J);
 // both phases at once (single MSMs)

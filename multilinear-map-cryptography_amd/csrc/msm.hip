@@ -33,6 +33,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <memory>
 #include <cstdlib>
 #include <vector>
 
@@ -583,8 +584,10 @@ struct MsmJob {
   // between the sort phase and the accumulation phase
   bool sorted = false;
   bool sort_pending = false;        // bucket_sort_begin done, msm_finish_sort not yet
+  bool passes_pending = false;      // bucket_sort_passes not yet queued
   BucketSortJob bs;
   hipEvent_t sorted_ev = nullptr;   // recorded on the lane once the bucket order exists
+  std::unique_ptr<ProfScope> sort_prof;  // "msm_sort" timing from pass 1 to the last pass
   const G1Affine *points = nullptr;
   uint32_t *keys2 = nullptr, *vals2 = nullptr, *bstart = nullptr, *bend = nullptr, *valid = nullptr;
   int ks = 0, acc_k = 0;
@@ -673,10 +676,11 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   J.nchunks = (total + acc_k - 1) / acc_k;
   J.n = n;
   if (!ctx->msm_cub_sort) {
-    TNS_PROF_ON(ctx, st, "msm_sort", 32.0 * n + 16.0 * total);
+    J.sort_prof.reset(new ProfScope(ctx->prof, st, "msm_sort", 32.0 * n + 16.0 * total));
     J.valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
     bucket_sort_begin(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
     J.sort_pending = true;
+    J.passes_pending = true;
     if (!defer) msm_finish_sort(J);
     return;
   }
@@ -711,11 +715,20 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   record_now();
 }
 
-// the bucket sort's second phase (waits for its last-pass readback), then the sorted state
+// the bucket sort's passes after pass 1, up to the last pass's readback (no host wait)
+static void msm_sort_passes(MsmJob &J) {
+  if (!J.passes_pending) return;
+  J.passes_pending = false;
+  bucket_sort_passes(J.bs);
+}
+
+// the bucket sort's last stage (waits for its last-pass readback), then the sorted state
 static void msm_finish_sort(MsmJob &J) {
   if (!J.sort_pending) return;
+  msm_sort_passes(J);
   J.sort_pending = false;
   const BucketOrder o = bucket_sort_finish(J.bs);
+  J.sort_prof.reset();  // the stage's end event, after the last pass on the lane
   J.keys2 = o.keys;
   J.vals2 = o.vals;
   J.bstart = o.bstart;
@@ -914,9 +927,15 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     // only after lane 0's sort completes, for A/B)
     const char *ov = getenv("TNS_SORT_OVERLAP");
     const bool overlap = !(ov && ov[0] == '0');
+    // TNS_SORT_INTERLEAVE=1: both lanes' pass 1 queued before either lane's later passes (A/B)
+    const char *il = getenv("TNS_SORT_INTERLEAVE");
+    const bool interleave = il && il[0] == '1';
     msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa, overlap);
     if (!overlap) msm_finish_sort(ja);
+    if (!interleave) msm_sort_passes(ja);
     msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, overlap);
+    msm_sort_passes(ja);
+    msm_sort_passes(jb);
     msm_finish_sort(ja);
     msm_finish_sort(jb);
   }
