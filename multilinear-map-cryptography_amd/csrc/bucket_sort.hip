@@ -528,6 +528,7 @@ void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, b
   if (W > BS_TILE) throw Error(TNS_ERR_COMMITMENT, "too many MSM windows");
   J = BucketSortJob();
   J.ln = &ln;
+  J.valid = valid;
   J.E = E;
   J.bucket_bits = bucket_bits;
   uint32_t **K = J.K, **V = J.V;
@@ -631,9 +632,11 @@ void bucket_sort_passes(BucketSortJob &J) {
     exclusive_scan(st, ln.ws[9], J.tcount, J.tbase, J.S + 1);
     if (J.last) {  // the readback; pass_rest runs after bucket_sort_finish's wait
       exclusive_scan(st, ln.ws[9], J.mcount, J.mbase, J.S + 1);
-      uint32_t *h = (uint32_t *)ln.host2.ensure(2 * sizeof(uint32_t));
+      uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
       TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      // the entry count (k_bs_segs1 wrote it): the accumulation sizes its chunks from it
+      TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       J.pending = true;
       return;
     }
@@ -686,9 +689,11 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
 
 BucketOrder bucket_sort_finish(BucketSortJob &J) {
   MsmLane &ln = *J.ln;
+  size_t entries = SIZE_MAX;  // unknown without the readback
   if (J.pending) {
     TNS_HIP(hipStreamSynchronize(ln.stream));  // the last pass's tile totals (host2)
     J.pending = false;
+    entries = ((const uint32_t *)ln.host2.p)[2];
     bucket_sort_pass_rest(J, true);
   }
   uint32_t *bstart = J.seg[J.cur];
@@ -698,7 +703,7 @@ BucketOrder bucket_sort_finish(BucketSortJob &J) {
     k_bs_bucket_starts<<<grid_for(nbk + 1, 256), 256, 0, ln.stream>>>(J.seg[J.cur], nbk, J.wb, bstart);
     TNS_LAUNCH_CHECK();
   }
-  return BucketOrder{J.K[J.cur], J.V[J.cur], bstart, J.wb};
+  return BucketOrder{J.K[J.cur], J.V[J.cur], bstart, J.wb, entries};
 }
 
 BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,

@@ -266,8 +266,9 @@ struct Ctx {
   // wave slots to a co-running sort; 0 (default) = one block per 256 chunks
   int num_cu = 256, acc_waves = 0;
   // sorted entries per k_accumulate thread (TNS_ACC_K fixes it; C4: 32 -> 62.0, 128 -> 61.1 ms).
-  // 0 = adaptive: 128, halved (down to 32) while the MSM would give fewer than acc_threads_cu
-  // threads per CU (small MSMs: enough waves per SIMD to hide the point gathers)
+  // 0 = adaptive (msm.hip acc_chunk): the largest chunk <= 128 filling whole rounds of resident
+  // blocks; TNS_ACC_ROUNDS=0: the round-1 rule, 128 halved (down to 32) while the MSM would give
+  // fewer than acc_threads_cu threads per CU
   int acc_k = 0, acc_threads_cu = 1024;
   int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
   int red_ch = 0;  // masked-sum chunk length (TNS_RED_CH, power of two; 0 = 16)
@@ -401,7 +402,8 @@ void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
 // bucket_sort.hip: the MSM's digit entries grouped by bucket (bucket k = [bstart[k], bstart[k+1]))
 struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
-  int ks;  // bucket = key >> ks
+  int ks;          // bucket = key >> ks
+  size_t entries;  // sorted entries (non-zero digits) when read back, else SIZE_MAX
 };
 // A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
 // pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
@@ -415,6 +417,7 @@ struct BucketSortJob {
   uint32_t *K[2] = {nullptr, nullptr}, *V[2] = {nullptr, nullptr}, *seg[2] = {nullptr, nullptr};
   uint32_t *counts = nullptr, *offs = nullptr, *tcount = nullptr, *tbase = nullptr, *desc = nullptr;
   uint32_t *mcount = nullptr, *mbase = nullptr;
+  uint32_t *valid = nullptr;  // device: the entry count
 };
 void bucket_sort_begin(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J);

@@ -588,6 +588,7 @@ struct MsmJob {
   BucketSortJob bs;
   hipEvent_t sorted_ev = nullptr;   // recorded on the lane once the bucket order exists
   std::unique_ptr<ProfScope> sort_prof;  // "msm_sort" timing from pass 1 to the last pass
+  Ctx *ctx = nullptr;
   const G1Affine *points = nullptr;
   uint32_t *keys2 = nullptr, *vals2 = nullptr, *bstart = nullptr, *bend = nullptr, *valid = nullptr;
   int ks = 0, acc_k = 0;
@@ -610,6 +611,33 @@ static unsigned bits_result(MsmLane &ln) {
   return *(unsigned *)ln.host.p;
 }
 
+// Entries per accumulation thread.  Per-window plans (the narrow commitments: runs of a few
+// entries, flush- and latency-bound): 128, halved down to 32 while the MSM gives fewer than
+// acc_threads_cu threads per CU -- short chunks shorten each thread's dependent chain.
+// Table-window plans (full-width scalars) whose count the sort read back: the largest chunk
+// <= 128 that fills whole rounds of the resident blocks (fewer chunks, fewer head/tail partials
+// for the fixup: C2 2.17 -> 2.11 ms; the 2^24 openings keep 128, `profiles/r02_ab_acc_rounds.txt`).
+// TNS_ACC_K forces a chunk; TNS_ACC_ROUNDS=0 / 1 forces the first / second rule.
+static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
+  if (ctx->acc_k > 0) return ctx->acc_k;
+  const char *ar = getenv("TNS_ACC_ROUNDS");
+  if (ar ? ar[0] == '0' : !table_plan) {
+    const size_t want = (size_t)ctx->num_cu * ctx->acc_threads_cu;
+    int k = 128;
+    while (k > 32 && entries / k < want) k /= 2;
+    return k;
+  }
+  static const int bpc = [] {  // resident blocks of 256 threads per CU (VGPR-bound: 3)
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_accumulate, 256, 0) != hipSuccess || b < 1) b = 3;
+    return b;
+  }();
+  const size_t slots = (size_t)ctx->num_cu * bpc * 256;
+  const size_t rounds = std::max<size_t>(1, (entries + 128 * slots - 1) / (128 * slots));
+  const size_t k = (entries + rounds * slots - 1) / (rounds * slots);
+  return (int)std::max<size_t>(16, std::min<size_t>(128, k));
+}
+
 // Phase 1 on lane `ln` (asynchronous): plan, digits and the bucket order.  Trivial cases
 // (all scalars zero, n <= 64) finish here.  `sorted` (optional) is recorded on the lane once
 // the bucket order exists (or right away when there is none).
@@ -621,6 +649,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
                             size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr,
                             bool defer = false) {
   J.lane = &ln;
+  J.ctx = ctx;
   J.sorted_ev = sorted;
   hipStream_t st = ln.stream;
   auto record_now = [&]() {
@@ -665,12 +694,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
-  int acc_k = ctx->acc_k;
-  if (acc_k <= 0) {
-    const size_t want = (size_t)ctx->num_cu * ctx->acc_threads_cu;
-    acc_k = 128;
-    while (acc_k > 32 && total / acc_k < want) acc_k /= 2;
-  }
+  const int acc_k = acc_chunk(ctx, total, false);  // from the bound; table plans refine it from the sort's count
   J.points = points;
   J.acc_k = acc_k;
   J.nchunks = (total + acc_k - 1) / acc_k;
@@ -729,6 +753,10 @@ static void msm_finish_sort(MsmJob &J) {
   J.sort_pending = false;
   const BucketOrder o = bucket_sort_finish(J.bs);
   J.sort_prof.reset();  // the stage's end event, after the last pass on the lane
+  if (o.entries != SIZE_MAX && J.P.shared) {  // table plans: chunks sized from the actual entry count
+    J.acc_k = acc_chunk(J.ctx, o.entries, true);
+    J.nchunks = std::max<size_t>(1, (o.entries + J.acc_k - 1) / J.acc_k);
+  }
   J.keys2 = o.keys;
   J.vals2 = o.vals;
   J.bstart = o.bstart;
