@@ -247,21 +247,35 @@ struct FixLevels {
   int n;                        // levels built (0: none)
 };
 
+// FIX_FAN consecutive lanes per group: lane j loads item j and the group's sum is an xor butterfly
+// over those lanes (3 dependent additions instead of one thread's chain of 7: the narrow value
+// commitment's heavy buckets fill thousands of groups and this level ran at half a wave per SIMD)
+static_assert(FIX_FAN == 8, "k_fix_level's butterfly assumes 8 lanes per group");
 __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ keys,
                                                    const uint32_t *__restrict__ valid_p,
                                                    const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
                                                    int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks,
                                                    int acc_k) {
   const size_t valid = *valid_p;
-  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < n_groups; g += (size_t)gridDim.x * blockDim.x) {
+  const int j = threadIdx.x & (FIX_FAN - 1);
+  const size_t stride = (size_t)gridDim.x * blockDim.x / FIX_FAN;
+  // group-uniform trip count (blockDim.x is a multiple of FIX_FAN): the 8 lanes of a group stay together
+  for (size_t g = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) / FIX_FAN; g < n_groups; g += stride) {
     size_t span = (size_t)acc_k;
     for (int l = 0; l < level; l++) span *= FIX_FAN;
     const size_t a = g * span, b = a + span;  // entries covered
-    if (b > valid || (keys[a] >> ks) != (keys[b - 1] >> ks)) continue;
-    G1Xyzz acc = level == 1 ? ht[g * FIX_FAN].head : below[g * FIX_FAN];
-    for (int i = 1; i < FIX_FAN; i++)
-      acc = xyzz_add_lazy(acc, level == 1 ? ht[g * FIX_FAN + i].head : below[g * FIX_FAN + i]);
-    out[g] = acc;
+    const bool uniform = b <= valid && (keys[a] >> ks) == (keys[b - 1] >> ks);
+    G1Xyzz acc = G1Xyzz::inf();
+    if (uniform) acc = level == 1 ? ht[g * FIX_FAN + j].head : below[g * FIX_FAN + j];
+    for (int off = FIX_FAN / 2; off > 0; off >>= 1) {  // every lane of the wave takes part
+      G1Xyzz o;
+      const uint32_t *pa = reinterpret_cast<const uint32_t *>(&acc);
+      uint32_t *po = reinterpret_cast<uint32_t *>(&o);
+#pragma unroll
+      for (int q = 0; q < (int)(sizeof(G1Xyzz) / 4); q++) po[q] = __shfl_xor(pa[q], off);
+      if (uniform) acc = xyzz_add_lazy(acc, o);
+    }
+    if (uniform && j == 0) out[g] = acc;
   }
 }
 
@@ -815,8 +829,8 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
       for (int l = 1; l <= F.n; l++) {
         F.lv[l] = base + o;
         o += F.len[l];
-        k_fix_level<<<grid_for(F.len[l], 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l, F.len[l],
-                                                                        F.lv[l], ks, acc_k);
+        k_fix_level<<<grid_for(F.len[l] * FIX_FAN, 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l,
+                                                                                  F.len[l], F.lv[l], ks, acc_k);
         TNS_LAUNCH_CHECK();
       }
     }
