@@ -647,9 +647,11 @@ static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
     return b;
   }();
   const size_t slots = (size_t)ctx->num_cu * bpc * 256;
-  const size_t rounds = std::max<size_t>(1, (entries + 128 * slots - 1) / (128 * slots));
+  size_t kmax = 128;  // TNS_ACC_TABLE_KMAX: the chunk cap of this rule (A/B)
+  if (const char *e = getenv("TNS_ACC_TABLE_KMAX")) kmax = std::max(16, atoi(e));
+  const size_t rounds = std::max<size_t>(1, (entries + kmax * slots - 1) / (kmax * slots));
   const size_t k = (entries + rounds * slots - 1) / (rounds * slots);
-  return (int)std::max<size_t>(16, std::min<size_t>(128, k));
+  return (int)std::max<size_t>(16, std::min<size_t>(kmax, k));
 }
 
 // Phase 1 on lane `ln` (asynchronous): plan, digits and the bucket order.  Trivial cases
