@@ -219,6 +219,8 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
       a.prep = s->prep;
       a.canon = s->canon;
       a.canon_bits = s->canon_bits;
+      a.u64 = s->u64;
+      a.n_u64 = s->n_u64;
     }
     return a;
   };
@@ -912,15 +914,15 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   }
   if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
-  // the address table (Montgomery for the sum-check and the openings, canonical with its bit
-  // length for the commitment's sort) is written on lane 0 as its MSM starts, so the value
-  // commitment's lane does not wait for it
-  Fr *A_canon = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * L);
+  // the address table (Montgomery, for the sum-check and the openings) and its bit length are
+  // written on lane 0 as its MSM starts, so the value commitment's lane does not wait for them;
+  // the commitment's sort reads the raw u64 addresses (8 bytes a scalar, no canonical copy)
   unsigned *a_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
   ScalarSource src_a;
-  src_a.prep = [=](hipStream_t s) { u64_tables_dev(s, ar, n_ops, L, A, A_canon, a_bits); };
-  src_a.canon = A_canon;
+  src_a.prep = [=](hipStream_t s) { u64_tables_dev(s, ar, n_ops, L, A, nullptr, a_bits); };
   src_a.canon_bits = a_bits;
+  src_a.u64 = ar;
+  src_a.n_u64 = n_ops;
   // ---- vector_to_polynomial + commit x2 (src/twist.rs:151-163).  The sum-check below
   // reads A and V without overwriting them, so the openings use the same vectors.
   Timer t_int;
@@ -1035,12 +1037,12 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   // the index table is written on lane 1 as the index commitment starts (see twist_core)
-  Fr *I_canon = (Fr *)c->prove_ws[8].ensure(sizeof(Fr) * LM);
   unsigned *i_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
   ScalarSource src_i;
-  src_i.prep = [=](hipStream_t s) { u64_tables_dev(s, ir, n_lookups, LM, I, I_canon, i_bits); };
-  src_i.canon = I_canon;
+  src_i.prep = [=](hipStream_t s) { u64_tables_dev(s, ir, n_lookups, LM, I, nullptr, i_bits); };
   src_i.canon_bits = i_bits;
+  src_i.u64 = ir;
+  src_i.n_u64 = n_lookups;
   Timer t_int;
   EvalPoly pt, pi;
   pt.N = T;

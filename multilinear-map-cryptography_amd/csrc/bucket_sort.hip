@@ -4,8 +4,8 @@
 // k_accumulate (msm.hip) needs the W*n (bucket, point|sign) entries of an MSM grouped by
 // bucket.  A general radix sort (rocPRIM onesweep) spends a digit kernel, a histogram pass
 // and one full read+write of keys and values per 8-bit digit on it.  Here:
-//  * pass 1 reads the SCALARS (canonical form, written by msm.hip's k_scalar_bits; 32 B for W
-//    entries), recomputes their digits in registers and scatters the entries straight into bins of the top key bits -- the
+//  * pass 1 reads the SCALARS (canonical, or Montgomery forms canonicalised on the fly, or raw
+//    u64 trace values; 32 or 8 B for W entries), recomputes their digits in registers and scatters the entries straight into bins of the top key bits -- the
 //    digit array never exists, and zero digits never enter the sort;
 //  * passes 2.. split each bin by the next key bits.  MSD order needs no stability, so a
 //    pass is per-tile LDS histograms + one exclusive scan + a scatter; tiles never cross a
@@ -46,14 +46,30 @@ struct DigitArgs {
   int c, W, wb;   // window bits, windows, window-index bits appended to the key (shared)
   bool shared;
   uint32_t stride;
+  bool mont;             // scalars are Montgomery forms: canonicalised here
+  const uint64_t *u64;   // set: raw u64 scalars instead (entries [0, n_u64), zero above)
+  size_t n_u64;
 };
+
+// scalar i of the digit pass, canonical
+__device__ __forceinline__ Fr load_scalar(const DigitArgs &A, size_t i) {
+  if (A.u64) {
+    const uint64_t x = i < A.n_u64 ? A.u64[i] : 0;
+    Fr k = Fr::zero();
+    k.v[0] = (uint32_t)x;
+    k.v[1] = (uint32_t)(x >> 32);
+    return k;
+  }
+  const Fr s = A.scalars[i];
+  return A.mont ? from_mont(s) : s;
+}
 
 // signed c-bit digits of scalar i (msm.hip k_digits): f(key, value) for every non-zero digit;
 // shared: key = (|d| - 1) << wb | w, value = (w * stride + i) | sign << 31
 // per-window: key = w << (c - 1) | (|d| - 1), value = i | sign << 31
 template <class F>
 __device__ __forceinline__ void scalar_digits(const Fr &s, size_t i, const DigitArgs &A, F f) {
-  const Fr &k = s;  // canonical (k_scalar_bits wrote them)
+  const Fr &k = s;  // canonical (load_scalar)
   uint32_t carry = 0;
   const int c = A.c;
   const uint32_t half = 1u << (c - 1);
@@ -92,7 +108,7 @@ __device__ __forceinline__ void tile_scalars(const DigitArgs &A, size_t a, size_
 #pragma unroll
     for (int j = 0; j < BS_SCALARS; j++) {
       const size_t i = i0 + (size_t)j * BS_BLOCK;
-      if (i < b) s[j] = A.scalars[i];
+      if (i < b) s[j] = load_scalar(A, i);
     }
 #pragma unroll
     for (int j = 0; j < BS_SCALARS; j++) {
@@ -224,7 +240,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shif
     Fr s[BS_SCALARS];  // the loads in flight together, then the digits
 #pragma unroll
     for (int j = 0; j < BS_SCALARS; j++)
-      if (i0 + (size_t)j * BS_BLOCK < b) s[j] = A.scalars[i0 + (size_t)j * BS_BLOCK];
+      if (i0 + (size_t)j * BS_BLOCK < b) s[j] = load_scalar(A, i0 + (size_t)j * BS_BLOCK);
 #pragma unroll
     for (int j = 0; j < BS_SCALARS; j++)
       if (i0 + (size_t)j * BS_BLOCK < b)
@@ -258,7 +274,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
 #pragma unroll
       for (int q = 0; q < LA; q++) {
         const size_t iq = a + threadIdx.x + (size_t)(j + q) * BS_BLOCK;
-        if (j + q < SPT && iq < b) s[q] = A.scalars[iq];
+        if (j + q < SPT && iq < b) s[q] = load_scalar(A, iq);
       }
     }
 #pragma unroll
@@ -520,7 +536,7 @@ static int pass_tile(int p) {
 // instead of lane a's ~20 (0.35 ms of launch overhead on the critical lane), and each lane's
 // last pass starts as soon as ITS readback lands (a single host wait would hold lane a's last
 // pass behind lane b's first two passes: ~1.7 ms of an idle lane per 2^24 opening pair).
-void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J) {
   hipStream_t st = ln.stream;
   const size_t E = (size_t)W * n;
@@ -536,7 +552,7 @@ void bucket_sort_begin(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, b
   K[1] = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * E);
   V[0] = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * E);
   V[1] = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * E);
-  DigitArgs A{scalars, n, 0, c, W, 0, shared, stride};
+  DigitArgs A{in.fr, n, 0, c, W, 0, shared, stride, in.mont, in.u64, in.n_u64};
   if (shared)
     while ((1 << A.wb) < W) A.wb++;
   J.wb = A.wb;
@@ -706,10 +722,10 @@ BucketOrder bucket_sort_finish(BucketSortJob &J) {
   return BucketOrder{J.K[J.cur], J.V[J.cur], bstart, J.wb, entries};
 }
 
-BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid) {
   BucketSortJob J;
-  bucket_sort_begin(ln, scalars, n, c, W, shared, stride, bucket_bits, valid, J);
+  bucket_sort_begin(ln, in, n, c, W, shared, stride, bucket_bits, valid, J);
   bucket_sort_passes(J);
   return bucket_sort_finish(J);
 }

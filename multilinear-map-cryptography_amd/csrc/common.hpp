@@ -339,8 +339,8 @@ Fr synthetic_division_dev(Ctx *c, const Fr *coeffs, size_t n, const Fr &z, Fr *q
 // g1_powers[first .. first + n) = G * tau^i
 void srs_generate_dev(Ctx *c, const Fr &tau, size_t first, size_t n, G1Affine *out);
 void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
-// u64 entries [0, n_in) zero-padded to n: Montgomery form (mont), canonical form (canon)
-// and the largest bit length (*bits, zeroed here) in one pass on stream s
+// u64 entries [0, n_in) zero-padded to n: Montgomery form (mont), canonical form (canon,
+// optional) and the largest bit length (*bits, zeroed here) in one pass on stream s
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
@@ -387,6 +387,9 @@ struct MsmArgs {
   // else `scalars` themselves (n > 64 only: the tiny path reads Montgomery scalars)
   const unsigned *canon_bits = nullptr;
   const Fr *canon = nullptr;
+  // set (with canon_bits): the sort reads these raw u64 values (entries [0, n_u64)) instead
+  const uint64_t *u64 = nullptr;
+  size_t n_u64 = 0;
   // enqueued on the lane's stream before anything else of this MSM: produces the scalars
   // (and canon / canon_bits) without holding up the other lane
   std::function<void(hipStream_t)> prep;
@@ -396,6 +399,8 @@ struct ScalarSource {
   std::function<void(hipStream_t)> prep;
   const Fr *canon = nullptr;
   const unsigned *canon_bits = nullptr;
+  const uint64_t *u64 = nullptr;
+  size_t n_u64 = 0;
 };
 // two independent MSMs overlapped on the context's two lanes (inputs ready on c->stream)
 void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
@@ -404,6 +409,15 @@ struct BucketOrder {
   uint32_t *keys, *vals, *bstart;
   int ks;          // bucket = key >> ks
   size_t entries;  // sorted entries (non-zero digits) when read back, else SIZE_MAX
+};
+// What the bucket sort's digit pass reads: canonical scalars, Montgomery scalars (converted in
+// the pass: no canonical copy is written), or raw u64 values (trace addresses, lookup indices:
+// 8 bytes a scalar instead of 32; entries [0, n_u64), zero above).
+struct SortInput {
+  const Fr *fr = nullptr;
+  bool mont = false;
+  const uint64_t *u64 = nullptr;
+  size_t n_u64 = 0;
 };
 // A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
 // pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
@@ -419,13 +433,13 @@ struct BucketSortJob {
   uint32_t *mcount = nullptr, *mbase = nullptr;
   uint32_t *valid = nullptr;  // device: the entry count
 };
-void bucket_sort_begin(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J);
 void bucket_sort_passes(BucketSortJob &J);
 void bucket_sort_pass_rest(BucketSortJob &J, bool readback);
 BucketOrder bucket_sort_finish(BucketSortJob &J);
 // both phases at once (single MSMs)
-BucketOrder bucket_sort_dev(MsmLane &ln, const Fr *canon_scalars, size_t n, int c, int W, bool shared, uint32_t stride,
+BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)

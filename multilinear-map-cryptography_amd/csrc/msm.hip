@@ -103,14 +103,14 @@ static void finish_plan(MsmPlan &p) {
   p.nb = (size_t)p.Wr * p.half;
 }
 
-// *bits = max over i of bitlen(canonical scalar_i); canon[i] = the canonical scalars (the
-// bucket sort's digit sweeps read these instead of converting the Montgomery form again)
+// *bits = max over i of bitlen(canonical scalar_i); canon (optional) = the canonical scalars
+// (the bucket sort canonicalises Montgomery scalars itself, so the MSMs pass none)
 __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scalars, size_t n,
                                                      unsigned *__restrict__ bits, Fr *__restrict__ canon) {
   unsigned b = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     Fr k = from_mont(scalars[i]);
-    canon[i] = k;
+    if (canon) canon[i] = k;
     b = max(b, fr_bit_length(k));
   }
   block_atomic_max2(b, 0u, bits, nullptr);
@@ -609,15 +609,19 @@ struct MsmJob {
   size_t nchunks = 0, n = 0;
 };
 
-static const Fr *bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
-  Fr *canon = (Fr *)ln.ws[16].ensure(sizeof(Fr) * n);
+// the largest bit length of Montgomery scalars; the sort then reads them as they are
+// (SortInput::mont: canonicalised in its digit pass instead of through a canonical copy)
+static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
   unsigned *d_bits = (unsigned *)ln.ws[4].ensure(sizeof(unsigned));
   unsigned *h_bits = (unsigned *)ln.host.ensure(sizeof(unsigned));
   TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), ln.stream));
-  k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, canon);
+  k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, nullptr);
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
-  return canon;
+  SortInput in;
+  in.fr = scalars;
+  in.mont = true;
+  return in;
 }
 
 static unsigned bits_result(MsmLane &ln) {
@@ -661,7 +665,7 @@ static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
 // defer: stop before the bucket sort's host wait (its last pass's readback); msm_finish_sort
 // completes it, so a pair of MSMs can queue both lanes' passes before either waits.
 static void msm_finish_sort(MsmJob &J);
-static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
+static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const SortInput &in,
                             size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr,
                             bool defer = false) {
   J.lane = &ln;
@@ -718,7 +722,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   if (!ctx->msm_cub_sort) {
     J.sort_prof.reset(new ProfScope(ctx->prof, st, "msm_sort", 32.0 * n + 16.0 * total));
     J.valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
-    bucket_sort_begin(ln, canon, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
+    bucket_sort_begin(ln, in, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
     J.sort_pending = true;
     J.passes_pending = true;
     if (!defer) msm_finish_sort(J);
@@ -884,9 +888,9 @@ static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = null
 }
 
 
-static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const Fr *canon,
+static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const SortInput &in,
                        size_t n, const FixedBase *fb, unsigned bits, MsmJob &J) {
-  msm_launch_sort(ctx, ln, points, scalars, canon, n, fb, bits, J);
+  msm_launch_sort(ctx, ln, points, scalars, in, n, fb, bits, J);
   msm_launch_reduce(ctx, J);
 }
 
@@ -920,13 +924,13 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
   if (n == 0) return G1Xyzz::inf();
   MsmLane &ln = ctx->lanes[0];
   unsigned bits = 254;
-  const Fr *canon = nullptr;
+  SortInput in;
   if (n > 64) {
-    canon = bits_launch(ln, scalars, n);
+    in = bits_launch(ln, scalars, n);
     bits = bits_result(ln);
   }
   MsmJob J;
-  msm_launch(ctx, ln, points, scalars, canon, n, fb, bits, J);
+  msm_launch(ctx, ln, points, scalars, in, n, fb, bits, J);
   return msm_complete(ctx, J);
 }
 
@@ -939,15 +943,23 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   TNS_HIP(hipStreamWaitEvent(l1.stream, ready, 0));
   (void)hipEventDestroy(ready);
   unsigned ba = 254, bb = 254;
-  const Fr *ca = nullptr, *cb = nullptr;
-  // canonical inputs (the opening quotients) come with their bit lengths on the device
-  auto start = [&](MsmLane &ln, const MsmArgs &x) -> const Fr * {
+  SortInput ca, cb;
+  // canonical inputs (the opening quotients) and raw u64 inputs (trace addresses, lookup
+  // indices) come with their bit lengths on the device
+  auto start = [&](MsmLane &ln, const MsmArgs &x) -> SortInput {
     if (x.prep) x.prep(ln.stream);
-    if (x.n <= 64) return nullptr;
+    if (x.n <= 64) return SortInput();
     if (!x.canon_bits) return bits_launch(ln, x.scalars, x.n);
     TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
                            ln.stream));
-    return x.canon ? x.canon : x.scalars;
+    SortInput in;
+    if (x.u64) {
+      in.u64 = x.u64;
+      in.n_u64 = x.n_u64;
+    } else {
+      in.fr = x.canon ? x.canon : x.scalars;
+    }
+    return in;
   };
   ca = start(l0, a);
   cb = start(l1, b);

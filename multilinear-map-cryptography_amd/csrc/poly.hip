@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(256) k_u64_tables(const uint64_t *__restrict__
     Fr k = Fr::zero();
     k.v[0] = (uint32_t)x;
     k.v[1] = (uint32_t)(x >> 32);
-    canon[i] = k;
+    if (canon) canon[i] = k;
     mont[i] = from_u64<FrCfg>(x);
     b = x ? max(b, 64u - (unsigned)__builtin_clzll(x)) : b;
   }
