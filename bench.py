@@ -1,26 +1,31 @@
 #!/usr/bin/env python3
-"""bench.py -- Twist prover ops/s (C4) + KZG MSM G1-scalar-pairs/s at 2^20 (C2) on MI355X.
+"""bench.py -- Twist prover ops/s (C4 / C5) + KZG MSM G1-scalar-pairs/s at 2^20 (C2) on MI355X.
 
 A "step" is one Twist::prove (src/twist.rs:107-252) of the synthetic read/write trace of
-ProtocolBenchmarks (src/benchmarks.rs:88-99) with the trace already resident in HBM:
-C4 = setup_params(22), MemoryTrace::new(2^22), 2^24 operations.  `value` is the
-Twist prover throughput (operations / second, metric as src/benchmarks.rs:26-28) of the
-whole job.  Multi-GPU runs (torchrun, one process per GPU) by default prove ONE trace of
-N * 2^24 operations sharded over the ranks (the C5 shape): every rank holds a
-2^24-op slice and the ranks exchange per-MSM partial sums, barycentric partials and fold
-values by allgather; value = the operations of that one proof / the max over ranks of the
-timed region (barrier + synchronize on both sides).  --independent instead proves one
-trace per rank with no exchange at all (value = operations summed over ranks / max time).
-Both are weak scaling: 2^24 operations per GPU.
+ProtocolBenchmarks (src/benchmarks.rs:88-99) with the trace already resident in HBM.
 
-Extra fields (rank 0, N = 1): C2 MSM pairs/s at 2^20 (setup_params(18), Fr::rand scalars
-from ChaCha20Rng([7;32])), C3 Shout lookups/s (2^20-entry table, 2^20 lookups), the per-
-stage device-time breakdown (every stage timed by HIP events on 2 untimed steps after the
-timed region), the roofline of the dominant kernel (HIP events around its launches, on the
-lane stream it runs on, inside the timed steps -- the only events there; algorithmic bytes
-from SURVEY.md 8(d)), and two CPU baselines on a
-bounded sample (oracle/fastcpu.c with the GPU path's algorithms, and the C oracle restating
-the reference algorithms).
+Workloads (BASELINE.json configs):
+  * N = 1 (default): C4 = setup_params(22), MemoryTrace::new(2^22), 2^24 operations.
+  * N > 1 (default): C5 = ONE proof of the 2^26-operation trace, setup_params(24), sharded over
+    the N ranks (one process per GPU, torchrun): every rank holds a 2^26/N-op slice of the trace,
+    of the Lagrange basis and of the SRS; the ranks exchange per-MSM partial sums, barycentric
+    partials and fold values by allgather.  Total work fixed at C5: "scaling": "strong".
+  * --strong: C5 at every N, including N = 1 (the same-work baseline of the strong curve);
+    --weak: 2^24 operations per GPU (one N * 2^24-op proof); --independent: one C4 proof per rank.
+`value` = operations of the proof(s) / the max over ranks of the timed region (barrier +
+synchronize on both sides).  `--gpus N` without WORLD_SIZE starts the N rank processes itself
+(torch.distributed.run on 127.0.0.1) before any GPU call; under torchrun WORLD_SIZE must equal N.
+
+Extra fields (rank 0, N = 1): the drop-in rate (Twist::prove on host buffers through the C ABI,
+PCIe included, over the same steps), the coefficient route (interpolation + coefficient KZG: the
+only route for an SRS without tau, src/utils.rs:107), C2 MSM pairs/s at 2^20 (setup_params(18),
+Fr::rand scalars from ChaCha20Rng([7;32])), C3 Shout lookups/s (2^20-entry table, 2^20 lookups),
+the per-stage device-time breakdown (every stage timed by HIP events on 2 untimed steps after the
+timed region), the roofline of the dominant kernel (HIP events around its launches, on the lane
+stream it runs on, inside the timed steps -- the only events there; algorithmic bytes from
+SURVEY.md 8(d)), and two CPU baselines on a bounded sample (oracle/fastcpu.c with the GPU path's
+algorithms on every host core the process may use, and the C oracle restating the reference
+algorithms).
 """
 
 import argparse
@@ -55,12 +60,22 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--log-ops", type=int, default=24, help="Twist trace length 2^k (C4: 24)")
+    ap.add_argument("--log-ops", type=int, default=None,
+                    help="operations of one proof, 2^k (default: C4 = 24 at N = 1, C5 = 26 at N > 1)")
+    mode = ap.add_mutually_exclusive_group()
+    mode.add_argument("--strong", action="store_true", help="C5 (one 2^26-op proof) at every N, N = 1 included")
+    mode.add_argument("--weak", action="store_true", help="2^24 operations per GPU: one N * 2^24-op proof")
     ap.add_argument("--no-extras", action="store_true", help="skip C2/C3 extras and the CPU baseline")
     ap.add_argument("--cpu-baseline-ops", type=int, default=256,
                     help="reference-algorithm oracle sample size (C1: 256)")
-    ap.add_argument("--cpu-fast-log-ops", type=int, default=20,
-                    help="fast CPU baseline sample: one proof of 2^k operations (setup_params(18): k <= 20)")
+    ap.add_argument("--cpu-fast-log-ops", type=int, default=22,
+                    help="fast CPU baseline sample: one proof of 2^k operations (setup_params(k - 2))")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="fast CPU baseline threads (0: every core the process's affinity allows)")
+    ap.add_argument("--dropin-steps", type=int, default=None,
+                    help="drop-in (host-buffer) proofs timed after the resident steps (default: --steps)")
+    ap.add_argument("--coef-steps", type=int, default=2,
+                    help="coefficient-route proofs timed at N = 1 (0: skip)")
     ap.add_argument("--commit-basis", choices=["lagrange", "coefficients"], default="lagrange",
                     help="prove via the setup's Lagrange-basis SRS (default) or via interpolation + "
                          "coefficient KZG (the reference's route); identical proofs")
@@ -81,8 +96,27 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args) -> int:
+    """--gpus N without WORLD_SIZE: start the N rank processes (torch.distributed.run, one process
+    per GPU, rendezvous on 127.0.0.1) as children -- before this process touches the GPU -- and
+    return their exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.rehearse_one_gpu else int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
@@ -191,39 +225,54 @@ def cpu_reference_algorithms(n_ops):
                       f"{dt:.2f} s"}
 
 
-def host_threads():
+def host_cores():
+    """(threads to use, note): every CPU the process's affinity allows, capped by the cgroup CPU
+    quota when one is set (the GPU box grants 16 CPUs of time to a 1-GPU job on a 256-CPU host)."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(16, n))  # the box's CPU share per GPU is 16 cores
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, f"affinity {aff} CPUs, cgroup quota {quota if quota else 'none'} CPUs"
 
 
-def cpu_baseline(ts, pp18, log_ops, gpu_check=True):
+def cpu_baseline(ts, ctx, log_ops, threads=0, gpu_check=True):
     """Fast CPU baseline (SURVEY 8(d) 'fast-CPU'): oracle/fastcpu.c proves Twist with the GPU
-    path's algorithms (Lagrange-basis KZG, Pippenger MSM, fold sum-check) on host threads.
-    Bounded sample: one 2^log_ops-op proof of the src/benchmarks.rs:88-99 trace over
-    setup_params(18); the basis [L_j(tau)]G is the device-built setup artefact (downloaded,
-    not timed).  The proof is checked against the GPU's proof of the same trace."""
+    path's algorithms (Lagrange-basis KZG, Pippenger MSM, fold sum-check) on every host core the
+    process may use.  Bounded sample: one 2^log_ops-op proof of the src/benchmarks.rs:88-99 trace
+    over setup_params(log_ops - 2); the basis [L_j(tau)]G is the device-built setup artefact
+    (downloaded, not timed).  The proof is checked against the GPU's proof of the same trace."""
     from oracle import coracle as co
 
     n = 1 << log_ops
     L = log_ops - 2
+    pp, _ = ts.setup_params(L, device=ctx.device)
+    pp.commitment_params.srs.prepare_lagrange(n)
     addr, val, isw = ts.bench_trace(1 << L, n)
-    lag = pp18.commitment_params.srs.lagrange_points(n)
+    lag = pp.commitment_params.srs.lagrange_points(n)
     w = co.bary_weights(n)
-    T = host_threads()
+    T, note = host_cores()
+    if threads > 0:
+        T = threads
     t0 = time.perf_counter()
-    st, proof = co.fast_twist_prove(lag, w, pp18.max_operations, addr, val, isw, T)
+    st, proof = co.fast_twist_prove(lag, w, pp.max_operations, addr, val, isw, T)
     dt = time.perf_counter() - t0
     assert st == 0
     out = {"value": round(n / dt, 1), "unit": "ops/s", "cores": T, "kind": "port",
-           "sample": f"Twist::prove of a 2^{log_ops}-op trace (src/benchmarks.rs:88-99, setup_params(18)) with the "
+           "sample": f"Twist::prove of a 2^{log_ops}-op trace (src/benchmarks.rs:88-99, setup_params({L})) with the "
                      f"GPU path's algorithms in C (oracle/fastcpu.c: Lagrange-basis KZG, Pippenger MSM, fold "
-                     f"sum-check) on {T} host threads; {dt:.2f} s",
+                     f"sum-check) on {T} host threads ({note}); {dt:.2f} s",
            "host_cpu": platform.processor() or platform.machine(), "host_nproc": os.cpu_count()}
     if gpu_check:
-        g = ts.Twist(pp18).prove_soa(addr, val, isw)
+        g = ts.Twist(pp).prove_soa(addr, val, isw)
         same = (g.address_commitment.commitment == proof["address_commitment"]
                 and g.value_commitment.commitment == proof["value_commitment"]
                 and [q.proof for q in g.opening_proofs] == proof["opening_proofs"]
@@ -232,17 +281,36 @@ def cpu_baseline(ts, pp18, log_ops, gpu_check=True):
     return out
 
 
+def timed_proofs(fn, steps, warmup):
+    for _ in range(warmup):
+        fn()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    return (time.perf_counter() - t0) / max(1, steps)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world, rank, local, pg = dist_setup(args)
     import twist_and_shout as ts
 
     ctx = ts.Context.get(local)
-    log_ops = args.log_ops
-    n_ops = 1 << log_ops  # per GPU
     sharded = world > 1 and not args.independent
-    n_total = world * n_ops if sharded else n_ops  # operations of one proof
-    L = (n_total.bit_length() - 1) - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
+    # operations of ONE proof: C4 (2^24) at N = 1, C5 (2^26, setup_params(24)) at N > 1
+    if args.log_ops is not None:
+        log_total = args.log_ops + (world.bit_length() - 1 if args.weak and sharded else 0)
+    elif args.weak:
+        log_total = 24 + (world.bit_length() - 1 if sharded else 0)
+    elif args.strong or sharded:
+        log_total = 26
+    else:
+        log_total = 24
+    n_total = 1 << log_total
+    n_ops = n_total // world if sharded else n_total  # per GPU
+    L = log_total - 2  # setup_params(L): max_operations = 2^(L+2); memory size 2^L
     ctx.set_commit_basis(args.commit_basis == "lagrange")
     ctx.set_msm_tables(not args.no_msm_tables)
     t_setup = time.perf_counter()
@@ -307,37 +375,56 @@ def main():
     total_ops = (n_total if sharded else world * n_ops) * args.steps
     value = total_ops / dt_max
     if sharded:
-        workload = (f"C5-style: ONE Twist::prove of a {n_total}-op trace (2^{log_ops} per GPU) sharded over "
-                    f"{world} GPUs, setup_params_shard({L}), slices resident in HBM")
+        workload = (f"{'C5' if log_total == 26 else 'C5-style'}: ONE Twist::prove of a 2^{log_total}-op trace "
+                    f"(src/benchmarks.rs:88-99) sharded over {world} GPUs (2^{log_total - (world.bit_length() - 1)} "
+                    f"ops each), setup_params_shard({L}), slices resident in HBM")
         parallelism = f"one proof sharded x{world} ({args.comm} allgather of partial sums)"
     else:
-        workload = f"C4: Twist::prove, 2^{log_ops}-op trace, setup_params({L}), trace resident in HBM"
-        parallelism = f"independent traces x{world}"
+        name = "C5 on one GPU" if log_total == 26 else ("C4" if log_total == 24 else f"2^{log_total} ops")
+        workload = f"{name}: Twist::prove, 2^{log_total}-op trace, setup_params({L}), trace resident in HBM"
+        parallelism = f"independent traces x{world}" if world > 1 else "single GPU"
+    scaling = "weak" if (args.weak or args.independent) else "strong"
 
     out = {
         "metric": METRIC, "value": round(value, 2), "unit": "ops/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt_max / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u256 (8x u32 Montgomery, BN254 Fr/Fq)",
+        "scaling": scaling, "vs_baseline": None, "dtype": "u256 (8x u32 Montgomery, BN254 Fr/Fq)",
         "data": "synthetic (src/benchmarks.rs:88-99 trace)",
-        "config": {"workload": workload, "log_ops": log_ops, "ops_per_gpu": n_ops, "ops_per_proof": n_total,
-                   "parallelism": parallelism},
+        "config": {"workload": workload, "log_ops": log_total, "ops_per_gpu": n_ops, "ops_per_proof": n_total,
+                   "parallelism": parallelism,
+                   "scaling_note": "N = 1 proves C4 (the metric's single-GPU config); N > 1 prove ONE C5 trace "
+                                   "(2^26 ops, total fixed: strong scaling); --strong proves C5 at N = 1 too, "
+                                   "--weak keeps 2^24 ops per GPU"},
         "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
         "commit_basis": args.commit_basis,
         "setup_ms": {"setup_params": round(t_setup * 1e3, 1), "lagrange_basis": round(t_lag * 1e3, 1)},
     }
     if rank == 0 and world == 1 and not args.no_extras:
+        # drop-in rate: Twist::prove on host buffers through the C ABI (PCIe and host-side SoA
+        # included), the same number of steps (SURVEY 8(d) measures prove() on host data)
+        k = args.dropin_steps if args.dropin_steps is not None else args.steps
+        if k > 0:
+            tw = ts.Twist(pp)
+            t_di = timed_proofs(lambda: tw.prove_soa(addr, val, isw), k, 1)
+            out["twist_ops_per_sec_dropin"] = round(n_ops / t_di, 2)
+            out["ms_per_step_dropin"] = round(t_di * 1e3, 3)
+            out["dropin_steps"] = k
+        # the coefficient route (interpolation + coefficient KZG): an SRS without tau takes it
+        if args.coef_steps > 0 and args.commit_basis == "lagrange":
+            ctx.set_commit_basis(False)
+            try:
+                t_cf = timed_proofs(prove, args.coef_steps, 1)
+            finally:
+                ctx.set_commit_basis(True)
+            out["twist_ops_per_sec_coefficient_route"] = round(n_ops / t_cf, 2)
+            out["ms_per_step_coefficient_route"] = round(t_cf * 1e3, 3)
         # C2: MSM 2^20 pairs (setup_params(18)); scalars = Fr::rand from ChaCha20Rng([7;32])
         pp18, _ = ts.setup_params(18, device=local)
         if args.commit_basis == "lagrange":
             pp18.commitment_params.srs.prepare_lagrange(1 << 20)
         n = 1 << 20
         sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
-        ts.msm_resident(pp18.commitment_params, sc, n)
-        reps = 10
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            ts.msm_resident(pp18.commitment_params, sc, n)
-        t_msm = (time.perf_counter() - t1) / reps
+        t_msm = timed_proofs(lambda: ts.msm_resident(pp18.commitment_params, sc, n), 10, 1)
         out["msm_pairs_per_sec_2^20"] = round(n / t_msm, 1)
         out["msm_ms_2^20"] = round(t_msm * 1e3, 3)
         # C3: Shout, 2^20 squares table, 2^20 lookups i % 2^20 (src/benchmarks.rs:167-177)
@@ -345,23 +432,16 @@ def main():
         entries = ts.fr_from_u64_array(np.arange(T, dtype=np.uint64) ** 2)
         idx = np.arange(T, dtype=np.uint64)
         d_e, d_i = ts.DeviceBuffer(ctx, entries), ts.DeviceBuffer(ctx, idx)
-        ts.shout_prove_resident(pp18, d_e, T, d_i, T)
-        t2 = time.perf_counter()
-        ts.shout_prove_resident(pp18, d_e, T, d_i, T)
-        t_sh = time.perf_counter() - t2
+        t_sh = timed_proofs(lambda: ts.shout_prove_resident(pp18, d_e, T, d_i, T), 5, 1)
         out["shout_lookups_per_sec_2^20"] = round(T / t_sh, 1)
         out["shout_ms_2^20"] = round(t_sh * 1e3, 3)
-        # PCIe-inclusive Twist (host buffers through the C ABI), for DESIGN.md
-        t3 = time.perf_counter()
-        ts.Twist(pp).prove_soa(addr, val, isw)
-        out["twist_ops_per_sec_pcie_inclusive"] = round(n_ops / (time.perf_counter() - t3), 2)
     if roof is not None:
         out["roofline"] = roof
         out["stages_ms_per_step"] = {k: round(v["ms"] / stage_steps, 3) for k, v in stages.items()}
         out["stages_timed_on"] = ("the timed steps" if args.profile_all_timed or args.stage_steps <= 0
                                   else f"{stage_steps} untimed steps after the timed region")
     if rank == 0 and world == 1 and not args.no_extras:
-        out["cpu_baseline"] = cpu_baseline(ts, pp18, args.cpu_fast_log_ops)
+        out["cpu_baseline"] = cpu_baseline(ts, ctx, args.cpu_fast_log_ops, args.cpu_threads)
         out["cpu_reference_algorithms"] = cpu_reference_algorithms(args.cpu_baseline_ops)
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -129,6 +129,10 @@ int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange);
  * window-shifted table (built once, W copies of the points) so that every window shares
  * one bucket set; 0 forces the per-window bucket layout.  Same results. */
 int tns_ctx_set_msm_tables(tns_ctx *ctx, int on);
+/* The MSM's bucket order: rocprim != 0 uses a digit array + rocPRIM radix sort instead of the
+ * fused digit/counting sort (default; TNS_MSM_SORT=cub at context creation does the same).
+ * Same results; A/B and test use. */
+int tns_ctx_set_msm_sort(tns_ctx *ctx, int rocprim);
 
 /* ---------------------------------------------------------------- KZG (src/commitments.rs) */
 /* CommitmentScheme::commit for KZGCommitment (src/commitments.rs:162-180).
@@ -308,7 +312,8 @@ int tns_shout_prove_sharded(tns_ctx *ctx, const tns_srs *srs, const tns_params *
 /* ---------------------------------------------------------------- kernel timing */
 /* HIP-event timing of the named stages on the context stream ("msm_accumulate",
  * "msm_sort", "msm_digits", "msm_reduce", "ntt_stage", "ntt_lds", "ntt_pointwise",
- * "interp_tile", "sumcheck_round", "open_scan").  Enabling resets the totals. */
+ * "interp_tile", "sumcheck_round", "open_scan").  Enabling resets the totals and the stage
+ * filter of tns_profile_only (call that after enabling). */
 int tns_profile_enable(tns_ctx *ctx, int on);
 /* Restrict the timing to one stage (NULL or "": every stage).  Each timed stage costs two HIP
  * events per launch; the bench times only its roofline kernel inside the timed steps. */

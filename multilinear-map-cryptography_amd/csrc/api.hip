@@ -46,6 +46,8 @@ Ctx::~Ctx() {
   for (auto &kv : bary_w) delete kv.second;
   if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
   if (side) (void)hipStreamDestroy(side);
+  if (copy) (void)hipStreamDestroy(copy);
+  if (copied) (void)hipEventDestroy(copied);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -217,6 +219,7 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
     MsmArgs a{p.basis->points.as<G1Affine>(), p.y, p.cnt, p.basis->fb};
     if (s) {
       a.prep = s->prep;
+      a.late = s->late;
       a.canon = s->canon;
       a.canon_bits = s->canon_bits;
       a.u64 = s->u64;
@@ -347,6 +350,8 @@ int tns_ctx_create(int device, tns_ctx **out) {
     TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking,
                                         x->c.msm_stagger ? prio_hi : prio_lo));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
+    TNS_HIP(hipStreamCreateWithFlags(&x->c.copy, hipStreamNonBlocking));
+    TNS_HIP(hipEventCreateWithFlags(&x->c.copied, hipEventDisableTiming));
     *out = x;
     return TNS_OK;
   });
@@ -507,6 +512,14 @@ int tns_ctx_set_msm_tables(tns_ctx *ctx, int on) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
     ctx->c.msm_tables = on != 0;
+    return TNS_OK;
+  });
+}
+
+int tns_ctx_set_msm_sort(tns_ctx *ctx, int rocprim) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    ctx->c.msm_cub_sort = rocprim != 0;
     return TNS_OK;
   });
 }
@@ -850,6 +863,45 @@ __global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, ui
     if (idx[i] >= bound) *bad = 1;
 }
 
+// A host-to-device copy of one input vector on the context's copy stream, from a helper thread:
+// hipMemcpyAsync from pageable memory blocks its caller until the data has landed, so the copy
+// runs beside the calling thread, which meanwhile queues the proof's first MSM (the other vector's
+// commitment).  wait(s) joins the thread and makes stream s wait for the copy; the destructor
+// joins and drains it on every exit, so no copy outlives the call reading caller memory.
+struct HostUpload {
+  Ctx *c = nullptr;
+  std::thread th;
+  hipError_t err = hipSuccess;
+  bool waited = false;
+  void start(Ctx *ctx, void *dst, const void *src, size_t bytes) {
+    c = ctx;
+    th = std::thread([this, dst, src, bytes]() {
+      err = hipSetDevice(c->device);
+      if (err == hipSuccess) err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->copy);
+      if (err == hipSuccess) err = hipEventRecord(c->copied, c->copy);
+    });
+  }
+  void wait(hipStream_t s) {
+    if (!c || waited) return;
+    th.join();
+    waited = true;
+    TNS_HIP(err);
+    TNS_HIP(hipStreamWaitEvent(s, c->copied, 0));
+  }
+  ~HostUpload() {
+    if (th.joinable()) th.join();
+    if (c) (void)hipStreamSynchronize(c->copy);
+  }
+};
+
+// On every exit of a prove call (an exception included): nothing this call queued on the side
+// stream (the flag table, the zero-closure folds: they read the caller's value / is_write
+// buffers in the device-resident entry points) is still running when the call returns.
+struct SideDrain {
+  Ctx *c;
+  ~SideDrain() { (void)hipStreamSynchronize(c->side); }
+};
+
 // Twist::prove (src/twist.rs:107-252) for this rank's slice of the trace: operations
 // [rank L, rank L + n_local) of n_total, L = next_pow2(n_total) / size.  kind: where
 // addr/value/is_write live (H2D or D2D).  size 1 = the unsharded prover.
@@ -873,6 +925,8 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
   TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
+  SideDrain drain{c};
+  HostUpload upload;  // host values: uploaded under the address commitment
   // ---- SoA extraction / padding into the resident workspace (src/twist.rs:115-148)
   Timer t_h2d;
   DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
@@ -895,7 +949,11 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     ar = dar;
     fl = dfl;
   }
-  if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
+  // host values (32 B an op, 4x the addresses): copied on the copy stream from a helper thread
+  // while the address commitment runs (commit_evals_pair: the value MSM is `late`)
+  const bool v_late = kind == hipMemcpyHostToDevice && n_ops > 0;
+  if (v_late) upload.start(c, V, value, sizeof(Fr) * n_ops);
+  else if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
   // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
   // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
@@ -937,7 +995,13 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];
-  commit_evals_pair(c, srs->s, pa, pv, m, cm, &src_a, nullptr);
+  ScalarSource src_v;
+  if (v_late) {
+    src_v.prep = [&upload](hipStream_t s) { upload.wait(s); };
+    src_v.late = true;
+  }
+  commit_evals_pair(c, srs->s, pa, pv, m, cm, &src_a, v_late ? &src_v : nullptr);
+  upload.wait(st);  // (done already unless a path above skipped the value MSM's prep)
   const G1Affine Ca = cm[0], Cv = cm[1];
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
@@ -1006,12 +1070,19 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   double *tm = ctx->timing;
   for (int i = 0; i < 6; i++) tm[i] = 0;
   TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
+  SideDrain drain{c};
+  HostUpload upload;  // host table entries: uploaded under the index commitment
   Timer t_h2d;
   DevBuf &d_idx_raw = c->prove_ws[0], &d_bad = c->prove_ws[1], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3],
          &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
   Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * LT), *I = (Fr *)d_i.ensure(sizeof(Fr) * LM);
-  fr_fill_zero_dev(c, TB, LT);
-  if (n_entries) TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
+  if (LT > n_entries) fr_fill_zero_dev(c, TB + n_entries, LT - n_entries);  // the padding (src/shout.rs:105-107)
+  const bool t_late = kind == hipMemcpyHostToDevice && n_entries > 0;
+  if (t_late) {
+    upload.start(c, TB, entries, sizeof(Fr) * n_entries);
+  } else if (n_entries) {
+    TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
+  }
   // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
   unsigned hbad = 0;
   const uint64_t *ir = indices;
@@ -1058,7 +1129,13 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   tm[1] = t_int.ms();
   Timer t_com;
   G1Affine cm[2];
-  commit_evals_pair(c, srs->s, pt, pi, m, cm, nullptr, &src_i);  // table first (src/shout.rs:125-133)
+  ScalarSource src_t;
+  if (t_late) {
+    src_t.prep = [&upload](hipStream_t s) { upload.wait(s); };
+    src_t.late = true;
+  }
+  commit_evals_pair(c, srs->s, pt, pi, m, cm, t_late ? &src_t : nullptr, &src_i);  // (src/shout.rs:125-133)
+  upload.wait(st);
   const G1Affine Ct = cm[0], Ci = cm[1];
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);
@@ -1437,6 +1514,7 @@ int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, 
 // ---------------------------------------------------------------- kernel timing (HIP events)
 int tns_profile_enable(tns_ctx *ctx, int on) {
   ctx->c.prof.enabled = on != 0;
+  ctx->c.prof.only.clear();  // a new profile times every stage until tns_profile_only narrows it
   ctx->c.prof.start(ctx->c.stream);
   return TNS_OK;
 }

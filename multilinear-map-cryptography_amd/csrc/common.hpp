@@ -245,6 +245,8 @@ struct Ctx {
   DevBuf sc_half[4], sc_chal, sc_out;  // the zero-closure fold chain on the side stream
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
+  hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)
+  hipEvent_t copied = nullptr;
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
@@ -393,10 +395,14 @@ struct MsmArgs {
   // enqueued on the lane's stream before anything else of this MSM: produces the scalars
   // (and canon / canon_bits) without holding up the other lane
   std::function<void(hipStream_t)> prep;
+  // the scalars are still arriving (a host upload in flight; prep waits for it): msm_pair_dev
+  // queues the other MSM whole before this one's prep
+  bool late = false;
 };
 // how one vector of commit_evals_pair gets ready (the MsmArgs fields of the same names)
 struct ScalarSource {
   std::function<void(hipStream_t)> prep;
+  bool late = false;
   const Fr *canon = nullptr;
   const unsigned *canon_bits = nullptr;
   const uint64_t *u64 = nullptr;

@@ -118,12 +118,21 @@ __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scal
 
 // shared = false: key = (w << (c-1)) | (|d| - 1), value = i | sign<<31
 // shared = true:  key = |d| - 1,                  value = (w * stride + i) | sign<<31
-__global__ void __launch_bounds__(256) k_digits(const Fr *__restrict__ scalars, size_t n, int c, int W,
+// The scalars as the sort's digit pass reads them (SortInput): Montgomery forms, canonical forms
+// (the opening quotients) or raw u64 values (trace addresses, lookup indices; zero above n_u64).
+__global__ void __launch_bounds__(256) k_digits(SortInput in, size_t n, int c, int W,
                                                 uint32_t sentinel, bool shared, uint32_t stride,
                                                 uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
-    Fr k = from_mont(scalars[i]);
+    Fr k = Fr::zero();
+    if (in.u64) {
+      const uint64_t x = i < in.n_u64 ? in.u64[i] : 0;
+      k.v[0] = (uint32_t)x;
+      k.v[1] = (uint32_t)(x >> 32);
+    } else {
+      k = in.mont ? from_mont(in.fr[i]) : in.fr[i];
+    }
     uint32_t carry = 0;
     const uint32_t half = 1u << (c - 1);
     for (int w = 0; w < W; w++) {
@@ -739,7 +748,13 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   J.ks = 0;
   {
     TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
-    k_digits<<<grid_for(n, 256), 256, 0, st>>>(scalars, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
+    // the sort's own input (a canonical or u64 SortInput must not be read as Montgomery forms)
+    SortInput din = in;
+    if (!din.fr && !din.u64) {
+      din.fr = scalars;
+      din.mont = true;
+    }
+    k_digits<<<grid_for(n, 256), 256, 0, st>>>(din, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
                                                keys, vals);
     TNS_LAUNCH_CHECK();
   }
@@ -935,6 +950,13 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
 }
 
 void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
+  if (a.late && !b.late) {  // the late vector goes second (lane 1)
+    G1Xyzz o[2];
+    msm_pair_dev(ctx, b, a, o);
+    out[0] = o[1];
+    out[1] = o[0];
+    return;
+  }
   MsmLane &l0 = ctx->lanes[0], &l1 = ctx->lanes[1];
   // lane 1 starts after everything already queued on the context stream (its inputs)
   hipEvent_t ready;
@@ -961,11 +983,27 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     }
     return in;
   };
+  MsmJob ja, jb;
+  if (b.late) {
+    // b's scalars are still being uploaded (HostUpload, a helper thread): a's MSM is queued whole
+    // first -- sort, accumulation, tail -- so it runs under the upload; b's prep then waits for
+    // the upload and b's MSM follows on lane 1
+    ca = start(l0, a);
+    if (a.n > 64) ba = bits_result(l0);
+    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja);
+    msm_launch_reduce(ctx, ja);
+    cb = start(l1, b);
+    if (b.n > 64) bb = bits_result(l1);
+    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb);
+    msm_launch_reduce(ctx, jb);
+    out[0] = msm_complete(ctx, ja);
+    out[1] = msm_complete(ctx, jb);
+    return;
+  }
   ca = start(l0, a);
   cb = start(l1, b);
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
-  MsmJob ja, jb;
   hipEvent_t sorted = nullptr, sa = nullptr, sb = nullptr;
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));

@@ -21,6 +21,7 @@ Errors raise ``TwistAndShoutError`` subclasses named after the Rust enum variant
 
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import threading
 from dataclasses import dataclass, field
@@ -121,6 +122,17 @@ def _g1_from_proj(limbs) -> G1Affine:
 
 
 # ----------------------------------------------------------------------------- device context
+_EXITING = False
+
+
+def _mark_exiting():
+    global _EXITING
+    _EXITING = True
+
+
+atexit.register(_mark_exiting)
+
+
 class Context:
     """One libtns context (HIP stream + workspaces) per device and process."""
 
@@ -141,10 +153,26 @@ class Context:
                 cls._by_device[device] = Context(device)
             return cls._by_device[device]
 
+    def __del__(self):
+        # a private context (sharded ranks, tests) frees its streams and workspaces with its last
+        # reference (its SRS objects and buffers hold one); never during interpreter shutdown,
+        # when the HIP runtime may already be gone
+        if _EXITING:
+            return
+        try:
+            N.load().tns_ctx_destroy(self.handle)
+        except Exception:
+            pass
+
     def set_commit_basis(self, lagrange: bool):
         """True (default): Twist/Shout commit and open through the SRS's Lagrange basis
         when it has tau; False: vector_to_polynomial + coefficient KZG.  Same proofs."""
         _check(N.load().tns_ctx_set_commit_basis(self.handle, 1 if lagrange else 0))
+
+    def set_msm_sort(self, rocprim: bool):
+        """False (default): fused digit + counting bucket sort; True: digit array + rocPRIM
+        radix sort (A/B).  Same results."""
+        _check(N.load().tns_ctx_set_msm_sort(self.handle, 1 if rocprim else 0))
 
     def set_msm_tables(self, on: bool):
         """True (default): MSMs over fixed bases use their window tables (one shared bucket
@@ -810,6 +838,44 @@ def _unpack_proof(pr: N.TnsProof, n_mles: int):
     )
 
 
+def _horner(coeffs: Sequence[int], x: int) -> int:
+    """field_utils::horner_eval (src/utils.rs:217-221): sum_i c_i x^i, any length (0 for none)."""
+    acc = 0
+    for c in reversed(list(coeffs)):
+        acc = (acc * x + c) % R_MOD
+    return acc
+
+
+def _verify_general(labels, commitments, rounds, final_eval, openings, finals, verifier_params) -> bool:
+    """Twist/Shout::verify (src/twist.rs:255-304, src/shout.rs:225-274) with SumCheck::verify
+    (src/sumcheck.rs:113-153) on the host, for proof shapes the C proof struct cannot hold: round
+    polynomials of any length (each is hashed into the transcript as it stands) and any number of
+    rounds.  Never raises on a malformed shape: it returns the reference's Ok(bool)."""
+    t = Transcript(verifier_params.fiat_shamir_seed)
+    t.append_field_element(labels[0], KZGCommitmentValue(commitments[0]).hash())
+    t.append_field_element(labels[1], KZGCommitmentValue(commitments[1]).hash())
+    claim = 0
+    for r, g in enumerate(rounds):
+        g = [int(c) % R_MOD for c in g]
+        if (_horner(g, 0) + _horner(g, 1)) % R_MOD != claim:
+            return False
+        t.append_field_elements(b"sumcheck_round_%d" % r, g)
+        claim = _horner(g, t.challenge_field_element(b"sumcheck_challenge_%d" % r))
+    if claim != int(final_eval) % R_MOD:
+        return False
+    ch = t.challenge_field_elements(b"opening_challenges", len(rounds))
+    if ch and len(openings) >= 2 and len(finals) >= 2:
+        vk = verifier_params.commitment_vk
+        for k in range(2):
+            if not KZGCommitment.verify(vk, KZGCommitmentValue(commitments[k]), ch[0], finals[k], KZGProof(openings[k])):
+                return False
+    return True
+
+
+def _c_struct_shape(rounds) -> bool:
+    return len(rounds) <= N.TNS_MAX_ROUNDS and all(len(g) == 4 for g in rounds)
+
+
 class Twist:
     """src/twist.rs:93-316 (prover)."""
 
@@ -838,6 +904,11 @@ class Twist:
     @staticmethod
     def verify(proof: TwistProof, verifier_params: VerifierParams) -> bool:
         """src/twist.rs:255-304 (host: sum-check replay + two pairing checks)."""
+        comms = [proof.address_commitment.commitment, proof.value_commitment.commitment]
+        if not _c_struct_shape(proof.consistency_proof.round_polynomials):
+            return _verify_general((b"address_commitment", b"value_commitment"), comms,
+                                   proof.consistency_proof.round_polynomials, proof.consistency_proof.final_evaluation,
+                                   [p.proof for p in proof.opening_proofs], proof.final_evaluations, verifier_params)
         pr = _pack_proof([proof.address_commitment.commitment, proof.value_commitment.commitment],
                          proof.consistency_proof.round_polynomials, proof.consistency_proof.final_evaluation,
                          [p.proof for p in proof.opening_proofs], proof.final_evaluations, verify=True)
@@ -938,6 +1009,11 @@ class Shout:
     @staticmethod
     def verify(proof: ShoutProof, verifier_params: VerifierParams) -> bool:
         """src/shout.rs:225-274"""
+        comms = [proof.table_commitment.commitment, proof.index_commitment.commitment]
+        if not _c_struct_shape(proof.lookup_proof.round_polynomials):
+            return _verify_general((b"table_commitment", b"index_commitment"), comms,
+                                   proof.lookup_proof.round_polynomials, proof.lookup_proof.final_evaluation,
+                                   [p.proof for p in proof.opening_proofs], proof.final_evaluations, verifier_params)
         pr = _pack_proof([proof.table_commitment.commitment, proof.index_commitment.commitment],
                          proof.lookup_proof.round_polynomials, proof.lookup_proof.final_evaluation,
                          [p.proof for p in proof.opening_proofs], proof.final_evaluations, verify=True)

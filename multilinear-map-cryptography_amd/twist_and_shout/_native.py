@@ -84,6 +84,7 @@ SIGNATURES = [
     ("tns_srs_lagrange_download", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, U64P]),
     ("tns_ctx_set_commit_basis", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_ctx_set_msm_tables", C.c_int, [C.c_void_p, C.c_int]),
+    ("tns_ctx_set_msm_sort", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_kzg_commit", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_kzg_open", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
     ("tns_kzg_commit_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),

@@ -238,3 +238,34 @@ def fast_twist_prove(lagrange, bary_w, max_ops, addr_u64, val_limbs, is_write, t
                               isw.ctypes.data_as(C.POINTER(C.c_uint8)), C.c_size_t(len(a)), C.c_int(threads),
                               C.byref(pr))
     return st, _proof_dict(pr, ("address_commitment", "value_commitment"))
+
+
+def bary_eval2(bary_w, y0_limbs, y1_limbs, x: int, threads=1):
+    """(f0(x), f1(x), ell(x)) as ints for two vectors of N evaluations on the nodes 0..N-1
+    (Montgomery limbs; y1 may be y0): the barycentric formula in O(N) on `threads` host threads
+    (fastcpu.c fc_bary_eval2).  Size-independent parity checks of commitments and openings
+    (C = f(tau) G, pi (tau - z) = C - v G).  x must not be a node."""
+    w = np.ascontiguousarray(bary_w, dtype=np.uint64).reshape(-1, 4)
+    y0 = np.ascontiguousarray(y0_limbs, dtype=np.uint64).reshape(-1, 4)
+    y1 = np.ascontiguousarray(y1_limbs, dtype=np.uint64).reshape(-1, 4)
+    assert len(w) == len(y0) == len(y1)
+    xl = fr_array([x])[0]
+    f0, f1, ell = (np.zeros(4, dtype=np.uint64) for _ in range(3))
+    st = lib().fc_bary_eval2(_p(w), _p(y0), _p(y1), C.c_size_t(len(w)), _p(xl), C.c_int(threads), _p(f0), _p(f1),
+                             _p(ell))
+    assert st == 0, "x is an interpolation node"
+    return fr_ints(f0)[0], fr_ints(f1)[0], fr_ints(ell)[0]
+
+
+def g1_mul_gen(k: int):
+    """k * G1 (affine ints, None = identity), by the C oracle's double-and-add."""
+    out = np.zeros(8, dtype=np.uint64)
+    lib().fc_g1_mul_gen(_p(fr_array([k % po.R_MOD])[0]), _p(out))
+    return g1_from_limbs(out)
+
+
+def g1_mul(P, k: int):
+    """k * P for an affine point P (ints, None = identity)."""
+    out = np.zeros(8, dtype=np.uint64)
+    lib().fc_g1_mul(_p(g1_to_limbs(P)), _p(fr_array([k % po.R_MOD])[0]), _p(out))
+    return g1_from_limbs(out)

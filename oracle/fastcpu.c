@@ -314,6 +314,57 @@ static void bary_range(void *vctx, size_t a, size_t b, int tid) {
   memcpy(J->s1 + 4 * tid, s1, 32);
 }
 
+/* f0(x), f1(x) of two evaluation vectors on the nodes 0..N-1 (y0 / y1: N x 4 Montgomery, y1 may
+ * equal y0), ell(x) = prod_j (x - j) and, when inv != NULL, inv[j] = 1 / (x - j): the barycentric
+ * form f(x) = ell(x) sum_j w_j y_j / (x - j) in O(N) (one batch inversion per thread range).
+ * Returns 1 when x is a node (outputs undefined), else 0. */
+static int bary_pair(const u64 *w, const u64 *y0, const u64 *y1, size_t N, const u64 x[4], int T, u64 *inv,
+                     u64 f0[4], u64 f1[4], u64 ell_out[4]) {
+  u64 *own = inv ? NULL : (u64 *)malloc(N * 32);
+  u64 *parts = (u64 *)calloc(3 * (size_t)T, 32);
+  bary_job bj = {x, w, y0, y1, inv ? inv : own, parts, parts + 4 * T, parts + 8 * T, 0};
+  par_for(N, T, bary_range, &bj);
+  u64 ell[4], s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  memcpy(ell, FR.one, 32);
+  for (int t = 0; t < T; t++) {
+    if (is_zero4(parts + 4 * t)) continue; /* a range no thread ran (ell parts are non-zero) */
+    fmul(&FR, ell, ell, parts + 4 * t);
+    fadd(&FR, s0, s0, parts + 4 * (T + t));
+    fadd(&FR, s1, s1, parts + 4 * (2 * T + t));
+  }
+  fmul(&FR, f0, ell, s0);
+  fmul(&FR, f1, ell, s1);
+  if (ell_out) memcpy(ell_out, ell, 32);
+  free(parts);
+  free(own);
+  return bj.bad;
+}
+
+int fc_bary_eval2(const uint64_t *bary_w, const uint64_t *y0, const uint64_t *y1, size_t N, const uint64_t x[4],
+                  int threads, uint64_t f0[4], uint64_t f1[4], uint64_t ell[4]) {
+  const int T = threads < 1 ? 1 : (threads > FC_MAX_THREADS ? FC_MAX_THREADS : threads);
+  return bary_pair(bary_w, y0, y1, N, x, T, NULL, f0, f1, ell);
+}
+
+void fc_g1_mul_gen(const uint64_t k[4], uint64_t out[8]) {
+  u64 gaff[8] = {0};
+  u64 one_c[4] = {1, 0, 0, 0}, two_c[4] = {2, 0, 0, 0};
+  to_mont(&FQ, gaff, one_c);
+  to_mont(&FQ, gaff + 4, two_c);
+  jac gen, P;
+  aff_to_jac(&gen, gaff);
+  jac_mul(&P, &gen, k);
+  jac_to_aff(out, &P);
+}
+
+void fc_g1_mul(const uint64_t aff[8], const uint64_t k[4], uint64_t out[8]) {
+  jac A, P;
+  if (is_zero4(aff) && is_zero4(aff + 4)) jac_zero(&A);
+  else aff_to_jac(&A, aff);
+  jac_mul(&P, &A, k);
+  jac_to_aff(out, &P);
+}
+
 typedef struct {
   const u64 *y0, *y1, *inv, *v0, *v1;
   u64 *q0, *q1;
@@ -388,23 +439,11 @@ int fc_twist_prove(const uint64_t *lagrange, const uint64_t *bary_w, size_t N, s
   }
   tr_free(&tr);
   /* barycentric values P(z) = ell(z) sum_j w_j y_j / (z - j), quotient node values, MSMs */
-  u64 *inv = (u64 *)malloc(N * 32), *parts = (u64 *)calloc(3 * (size_t)T, 32);
-  bary_job bj = {z, bary_w, YA, YV, inv, parts, parts + 4 * T, parts + 8 * T, 0};
-  par_for(N, T, bary_range, &bj);
+  u64 *inv = (u64 *)malloc(N * 32);
   int st = 0;
-  if (bj.bad) {
+  if (bary_pair(bary_w, YA, YV, N, z, T, inv, out->final_evaluations[0], out->final_evaluations[1], NULL)) {
     st = 2; /* z on a node (probability ~2^-230): not handled by this baseline */
   } else {
-    u64 ell[4], s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-    memcpy(ell, FR.one, 32);
-    for (int t = 0; t < T; t++) {
-      if (is_zero4(parts + 4 * t)) continue; /* a range no thread ran (ell parts are non-zero) */
-      fmul(&FR, ell, ell, parts + 4 * t);
-      fadd(&FR, s0, s0, parts + 4 * (T + t));
-      fadd(&FR, s1, s1, parts + 4 * (2 * T + t));
-    }
-    fmul(&FR, out->final_evaluations[0], ell, s0);
-    fmul(&FR, out->final_evaluations[1], ell, s1);
     quot_job qj = {YA, YV, inv, out->final_evaluations[0], out->final_evaluations[1], A, V};
     par_for(N, T, quot_range, &qj);
     fc_msm(lagrange, A, N, T, out->opening_proofs[0]);
@@ -412,7 +451,6 @@ int fc_twist_prove(const uint64_t *lagrange, const uint64_t *bary_w, size_t N, s
     out->num_openings = 2;
   }
   free(inv);
-  free(parts);
   for (int t = 0; t < 3; t++) free(tmp[t]);
   free(A);
   free(V);

@@ -18,6 +18,14 @@ extern "C" {
 void fc_bary_weights(size_t N, uint64_t *w);
 /* [L_j(tau)]G, j < N (N x 8), by scalar multiplication -- small N (tests) */
 void fc_lagrange_basis(const uint64_t tau[4], size_t N, uint64_t *out);
+/* f0(x), f1(x) for two vectors of N evaluations on the nodes 0..N-1 (Montgomery, N x 4; y1 may
+ * be y0) by the barycentric formula in O(N) on `threads` host threads, and ell(x) = prod (x - j).
+ * Returns 1 when x is a node.  Size-independent parity checks (C = f(tau) G, pi (tau - z) = C - v G). */
+int fc_bary_eval2(const uint64_t *bary_w, const uint64_t *y0, const uint64_t *y1, size_t N, const uint64_t x[4],
+                  int threads, uint64_t f0[4], uint64_t f1[4], uint64_t ell[4]);
+/* k G1 (k Montgomery Fr) and k P (P affine), affine out (identity = zeros) */
+void fc_g1_mul_gen(const uint64_t k[4], uint64_t out[8]);
+void fc_g1_mul(const uint64_t aff[8], const uint64_t k[4], uint64_t out[8]);
 /* Twist::prove of n_ops operations (N = next_pow2(n_ops) >= 2): addr as u64, val Montgomery
  * Fr, is_write bytes; lagrange = [L_j(tau)]G and bary_w = fc_bary_weights(N).  threads: host
  * threads to use.  Returns 0, 1 (InvalidParameters) or 2 (opening point on a node). */

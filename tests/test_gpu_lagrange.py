@@ -6,8 +6,6 @@ evaluations through [L_j(tau)]G; these tests pin that path to the oracle's
 interpolate-then-commit restatement and to the device coefficient path, including its
 fallbacks (uploaded SRS without tau, tau a node, challenge z a node).
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -130,33 +128,6 @@ def test_twist_proof_identical_on_both_paths(logn):
     finally:
         ctx.set_commit_basis(True)
     assert a == b
-
-
-@pytest.mark.parametrize("logn", [18, 20, 24])
-def test_twist_long_barycentric_chains_match_fast_cpu(logn):
-    """From 2^18 nodes the barycentric batch inversion runs 131072 chains of >= 2 nodes each (the
-    smaller parity cases have one node per chain): the GPU proof equals oracle/fastcpu.c's (the
-    reference algorithms' fast restatement, pinned in test_fastcpu.py) on the device's Lagrange
-    basis, and at 2^18 the address commitment also passes the trapdoor check C = f(tau) G."""
-    n = 1 << logn
-    L = logn - 2
-    pp, _ = params(L)
-    pp.commitment_params.srs.prepare_lagrange(n)
-    addr, val, isw = ts.bench_trace(1 << L, n)
-    g = ts.Twist(pp).prove_soa(addr, val, isw)
-    lag = pp.commitment_params.srs.lagrange_points(n)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))  # 2^24 (C4 itself): ~30 s on 16 threads
-    st, want = co.fast_twist_prove(lag, co.bary_weights(n), pp.max_operations, addr, val, isw, threads)
-    assert st == 0
-    assert g.address_commitment.commitment == want["address_commitment"]
-    assert g.value_commitment.commitment == want["value_commitment"]
-    assert g.opening_point == want["opening_point"]
-    assert [q.proof for q in g.opening_proofs] == want["opening_proofs"]
-    assert g.final_evaluations == want["final_evaluations"]
-    if logn == 18:
-        tau = pp.commitment_params.tau
-        f_tau = po.barycentric_eval([int(a) for a in addr], tau)
-        assert g.address_commitment.commitment == po.affine_mul(po.G1_GEN, f_tau)
 
 
 def test_chain_inverse_batch_matches_fermat(monkeypatch):

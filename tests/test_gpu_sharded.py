@@ -175,3 +175,60 @@ def test_rccl_communicator_one_rank():
     comm = ts.Comm.rccl(ctx, 0, 1, ts.Comm.unique_id())
     pp, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
     assert ts.Twist(pp).prove_sharded(comm, addr, val, isw, len(addr)) == want
+
+
+def test_c5_one_2e26_proof_over_8_ranks():
+    """BASELINE C5: ONE Twist::prove of the 2^26-operation ProtocolBenchmarks trace,
+    setup_params(24), sharded over 8 ranks (threads on one GPU here, one process per GPU in
+    bench.py): every rank returns the unsharded proof, and that proof passes the trapdoor
+    identities (C = f(tau) G, pi (tau - z) = C - v G, v = f(z); f by the C oracle's O(N)
+    barycentric evaluation) and the transcript replay."""
+    from test_gpu_configs import check_pair, replay
+
+    logn, size = 26, 8
+    n, L = 1 << logn, logn - 2
+    addr, val, isw = ts.bench_trace(1 << L, n)
+    ctx = ts.Context(0)  # private: its SRS, window table and workspaces go with it
+    pp, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
+    want = ts.Twist(pp).prove_soa(addr, val, isw)
+    seed, tau = pp.fiat_shamir_seed, pp.commitment_params.tau
+    del pp, ctx
+    got, errs = sharded_twist(L, size, addr, val, isw)
+    assert errs == [None] * size
+    assert all(p == want for p in got)
+    Ca, Cv = want.address_commitment.commitment, want.value_commitment.commitment
+    chals, z = replay(seed, (b"address_commitment", b"value_commitment"), Ca, Cv, logn)
+    assert want.sumcheck_challenges == chals and want.opening_point == z
+    assert want.consistency_proof.round_polynomials == [[0, 0, 0, 0]] * logn
+    check_pair(tau, n, ts.fr_from_u64_array(addr), val, (Ca, Cv), z, want.final_evaluations,
+               [p.proof for p in want.opening_proofs])
+
+
+@pytest.mark.skipif(ts.device_count() < 2, reason="needs 2 visible GPUs")
+def test_rccl_communicator_two_devices():
+    """The library's own RCCL communicator (ncclAllGather over xGMI) with 2 ranks on 2 GPUs,
+    one thread per rank: the sharded proof equals the unsharded one."""
+    L, size = 10, 2
+    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
+    want = ts.Twist(params(L)).prove_soa(addr, val, isw)
+    uid = ts.Comm.unique_id()
+    out, errs = [None] * size, [None] * size
+
+    def worker(r):
+        try:
+            ctx = ts.Context(r)
+            comm = ts.Comm.rccl(ctx, r, size, uid)
+            pp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+            first, count = ts.shard_slice(len(addr), r, size)
+            out[r] = ts.Twist(pp).prove_sharded(comm, addr[first:first + count], val[first:first + count],
+                                                isw[first:first + count], len(addr))
+        except BaseException as e:  # noqa: BLE001 -- surfaced below
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(size)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert errs == [None] * size
+    assert all(p == want for p in out)

@@ -172,16 +172,46 @@ def test_verify_opening_counts_follow_reference(golden, vk):
     assert ts.Shout.verify(sfew, _vp(vk))
 
 
-def test_malformed_proofs_raise(golden, vk):
+def test_unusual_proof_shapes_verify_like_the_reference(golden, vk):
+    """Round polynomials of other lengths and more than TNS_MAX_ROUNDS rounds: the reference's
+    verify (src/sumcheck.rs:113-153, src/twist.rs:255-304) never errors on them -- it hashes each
+    polynomial as it stands and returns Ok(bool) -- and neither does the mirror (host path);
+    every verdict equals the oracle's protocol_verify."""
+    key, tau = vk
+    ovk = po.verifier_key({"tau": tau})
     case = golden["twist"]["demo_L3"]
-    bad = _twist_proof(case)
-    bad.consistency_proof.round_polynomials[0] = [0, 0, 0]
-    with pytest.raises(ts.InvalidParameters):
-        ts.Twist.verify(bad, _vp(vk))
-    bad = _twist_proof(case)
-    bad.consistency_proof.round_polynomials = [[0, 0, 0, 0]] * 41
-    with pytest.raises(ts.InvalidParameters):
-        ts.Twist.verify(bad, _vp(vk))
+
+    def both(pr):
+        args = ([pr.address_commitment.commitment, pr.value_commitment.commitment],
+                pr.consistency_proof.round_polynomials, pr.consistency_proof.final_evaluation,
+                [q.proof for q in pr.opening_proofs], pr.final_evaluations)
+        want = po.protocol_verify(ovk, bytes(32), (b"address_commitment", b"value_commitment"), *args)
+        got = ts.Twist.verify(pr, _vp(vk))
+        assert got == want
+        return got
+
+    three = _twist_proof(case)
+    three.consistency_proof.round_polynomials[0] = [0, 0, 0]  # a different transcript: the openings fail
+    assert not both(three)
+    three.opening_proofs = []  # ... and with no openings to check it verifies, as in the reference
+    assert both(three)
+    many = _twist_proof(case)
+    many.consistency_proof.round_polynomials = [[0, 0, 0, 0]] * 41
+    assert not both(many)
+    many.final_evaluations = many.final_evaluations[:1]
+    assert both(many)
+    five = _twist_proof(case)
+    five.consistency_proof.round_polynomials[1] = [0, 0, 0, 0, 0]
+    five.opening_proofs = []
+    assert both(five)
+    five.consistency_proof.round_polynomials[1] = [1, R - 2, 0, 0, 0]  # g(0) + g(1) = 0, g != 0
+    assert both(five) == po.protocol_verify(ovk, bytes(32), (b"address_commitment", b"value_commitment"),
+                                            [five.address_commitment.commitment, five.value_commitment.commitment],
+                                            five.consistency_proof.round_polynomials, 0, [], [])
+
+
+def test_wire_format_opening_counts(golden):
+    case = golden["twist"]["demo_L3"]
     bad = _twist_proof(case)
     bad.opening_proofs = bad.opening_proofs[:1]
     with pytest.raises(ts.InvalidParameters):  # the wire format holds 0 or 2 openings
