@@ -163,6 +163,50 @@ __global__ void k_fill(Fr *a, size_t n, uint32_t seed) {
   }
 }
 
+// k_finish2<true> with a record of the first two iterations of chain t == 0 (dbg[0..7]:
+// iv0, pre_i, inv_i, d, iv1 for iteration 0; then pre_i, inv_i, d for iteration 1)
+__global__ void __launch_bounds__(256) k_finish2_dbg(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
+                                                     const Fr *__restrict__ c, const Fr *__restrict__ w,
+                                                     const Fr *__restrict__ y0, const Fr *__restrict__ y1, Fr *invs,
+                                                     Fr *__restrict__ sp, Fr *__restrict__ dbg) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const size_t cnt = (n - 1 - t) / T;
+  size_t i = t + cnt * T;
+  Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
+  Fr iv = c[t];
+  Fr s0 = Fr::zero(), s1 = Fr::zero();
+  int it = 0;
+  if (t == 0) dbg[0] = iv;
+  for (;;) {
+    const Fr p = pre[i];
+    const Fr inv_i = mul(iv, p);
+    if (t == 0 && it < 2) {
+      dbg[1 + 4 * it] = p;
+      dbg[2 + 4 * it] = inv_i;
+      dbg[3 + 4 * it] = d;
+    }
+    iv = mul(iv, d);
+    if (t == 0 && it < 2) dbg[4 + 4 * it] = iv;
+    it++;
+    invs[i] = inv_i;
+    const Fr wi = mul(w[i], inv_i);
+    s0 = add(s0, mul(wi, y0[i]));
+    s1 = add(s1, mul(wi, y1[i]));
+    if (i < T) break;
+    i -= T;
+    d = add(d, Tm);
+  }
+  sp[t] = s0;
+  sp[T + t] = s1;
+}
+
+static std::string hex(const Fr &v) {
+  char b[80];
+  for (int k = 0; k < 8; k++) sprintf(b + 8 * k, "%08x", v.v[7 - k]);
+  return std::string(b);
+}
+
 int main() {
   const size_t T = 131072;
   Fr x;  // an arbitrary Montgomery-form element < r
@@ -243,11 +287,47 @@ int main() {
           printf("  i=%zu: icp-variant %s, inv-variant %s\n", i, a1[i] == want ? "right" : "WRONG",
                  a2[i] == want ? "right" : "WRONG");
         }
-        auto hex = [](const Fr &v) {
-          static char b[80];
-          for (int k = 0; k < 8; k++) sprintf(b + 8 * k, "%08x", v.v[7 - k]);
-          return std::string(b);
-        };
+        {  // the failing kernel's intermediate values for chain 0 against the host
+          Fr *dd, *p3, *sp3;
+          CK(hipMalloc(&dd, sizeof(Fr) * 16));
+          CK(hipMalloc(&p3, sizeof(Fr) * n));
+          CK(hipMalloc(&sp3, sizeof(Fr) * 2 * Tn));
+          CK(hipMemcpy(p3, p1, sizeof(Fr) * n, hipMemcpyDeviceToDevice));  // p1 holds pre again
+          k_finish2_dbg<<<nb, 256>>>(x, n, Tn, Tm, p3, icpA, w, y0, y1, p3, sp3, dd);
+          CK(hipDeviceSynchronize());
+          Fr g[16];
+          CK(hipMemcpy(g, dd, sizeof(Fr) * 9, hipMemcpyDeviceToHost));
+          const Fr d0 = sub(x, from_u64<FrCfg>((uint64_t)T)), iv0 = hi[0];
+          const Fr iv1 = mul(iv0, d0), d1 = add(d0, Tm);
+          printf("  dbg it0: iv0 %d pre %d inv %d d %d iv1 %d | it1: pre %d inv %d d %d iv2 %d\n", g[0] == iv0,
+                 g[1] == pre[T], g[2] == mul(iv0, pre[T]), g[3] == d0, g[4] == iv1, g[5] == pre[0],
+                 g[6] == mul(iv1, pre[0]), g[7] == d1, g[8] == mul(iv1, d1));
+          std::vector<Fr> a3(n);
+          CK(hipMemcpy(a3.data(), p3, sizeof(Fr) * n, hipMemcpyDeviceToHost));
+          size_t dd3 = 0;
+          for (size_t i = 0; i < n; i++) dd3 += a3[i] != a2[i];
+          printf("  dbg kernel inverses differing from the inv(cp) kernel: %zu\n", dd3);
+          // the failing kernel's inverse of node 0 (second iteration of chain 0) against candidates
+          const Fr bad = a1[0], good = a2[0], one = Fr::one();
+          printf("  node0 bad  %s\n  node0 good %s\n", hex(bad).c_str(), hex(good).c_str());
+          const Fr cands[] = {iv0, mul(iv0, d0), mul(iv0, d1), mul(iv1, d1), mul(iv1, pre[T]), mul(iv0, pre[T]),
+                              mul(mul(iv1, d1), one), add(iv1, Tm), sub(iv1, Tm), mul(iv0, x), mul(iv1, x)};
+          for (int k = 0; k < (int)(sizeof cands / sizeof cands[0]); k++)
+            if (cands[k] == bad) printf("  node0 bad == candidate %d\n", k);
+          int same = 0;
+          for (int k = 0; k < 8; k++) same += bad.v[k] == good.v[k];
+          printf("  node0 limbs equal to the right value: %d of 8\n", same);
+          // and node T (first iteration) plus a few more chains
+          size_t firsts_bad = 0, seconds_bad = 0;
+          for (size_t t = 0; t < Tn; t++) {
+            firsts_bad += a1[t + T] != a2[t + T];
+            seconds_bad += a1[t] != a2[t];
+          }
+          printf("  chains with a wrong last node %zu, wrong first node %zu\n", firsts_bad, seconds_bad);
+          (void)hipFree(dd);
+          (void)hipFree(p3);
+          (void)hipFree(sp3);
+        }
         printf("  cp[0]   %s\n  icp[0]  %s\n  inv(cp) %s\n  pre[0] %s pre[T] %s\n", hex(hc[0]).c_str(),
                hex(hi[0]).c_str(), hex(inv(hc[0])).c_str(), hex(pre[0]).c_str(), hex(pre[T]).c_str());
       }
