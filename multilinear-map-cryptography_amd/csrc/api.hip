@@ -47,7 +47,8 @@ Ctx::~Ctx() {
   if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
   if (side) (void)hipStreamDestroy(side);
   if (copy) (void)hipStreamDestroy(copy);
-  if (copied) (void)hipEventDestroy(copied);
+  for (hipEvent_t e : stage_ev)
+    if (e) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -351,7 +352,6 @@ int tns_ctx_create(int device, tns_ctx **out) {
                                         x->c.msm_stagger ? prio_hi : prio_lo));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.copy, hipStreamNonBlocking));
-    TNS_HIP(hipEventCreateWithFlags(&x->c.copied, hipEventDisableTiming));
     *out = x;
     return TNS_OK;
   });
@@ -863,37 +863,6 @@ __global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, ui
     if (idx[i] >= bound) *bad = 1;
 }
 
-// A host-to-device copy of one input vector on the context's copy stream, from a helper thread:
-// hipMemcpyAsync from pageable memory blocks its caller until the data has landed, so the copy
-// runs beside the calling thread, which meanwhile queues the proof's first MSM (the other vector's
-// commitment).  wait(s) joins the thread and makes stream s wait for the copy; the destructor
-// joins and drains it on every exit, so no copy outlives the call reading caller memory.
-struct HostUpload {
-  Ctx *c = nullptr;
-  std::thread th;
-  hipError_t err = hipSuccess;
-  bool waited = false;
-  void start(Ctx *ctx, void *dst, const void *src, size_t bytes) {
-    c = ctx;
-    th = std::thread([this, dst, src, bytes]() {
-      err = hipSetDevice(c->device);
-      if (err == hipSuccess) err = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->copy);
-      if (err == hipSuccess) err = hipEventRecord(c->copied, c->copy);
-    });
-  }
-  void wait(hipStream_t s) {
-    if (!c || waited) return;
-    th.join();
-    waited = true;
-    TNS_HIP(err);
-    TNS_HIP(hipStreamWaitEvent(s, c->copied, 0));
-  }
-  ~HostUpload() {
-    if (th.joinable()) th.join();
-    if (c) (void)hipStreamSynchronize(c->copy);
-  }
-};
-
 // On every exit of a prove call (an exception included): nothing this call queued on the side
 // stream (the flag table, the zero-closure folds: they read the caller's value / is_write
 // buffers in the device-resident entry points) is still running when the call returns.
@@ -926,7 +895,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   for (int i = 0; i < 6; i++) tm[i] = 0;
   TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
   SideDrain drain{c};
-  HostUpload upload;  // host values: uploaded under the address commitment
+  HostUpload upload(c);  // host inputs: addresses, flags, then values (under the address commitment)
   // ---- SoA extraction / padding into the resident workspace (src/twist.rs:115-148)
   Timer t_h2d;
   DevBuf &d_addr_raw = c->prove_ws[0], &d_flags = c->prove_ws[1], &d_a = c->prove_ws[2],
@@ -939,21 +908,26 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   Fr *V = v_in_place ? (Fr *)const_cast<uint64_t *>(value) : (Fr *)d_v.ensure(sizeof(Fr) * L);
   const uint64_t *ar = addr;
   const uint8_t *fl = is_write;
+  // host inputs go through HostUpload (upload.cpp) on the copy stream, in the order the proof
+  // needs them: the addresses (the first commitment starts on them), the flags, then the values
+  // (32 B an op, 4x the addresses), whose copy runs under the address commitment -- the value MSM
+  // is `late` in commit_evals_pair and waits for it
+  const bool v_late = kind == hipMemcpyHostToDevice && n_ops > 0;
+  int up_a = -1, up_f = -1, up_v = -1;
   if (kind == hipMemcpyHostToDevice) {
     uint64_t *dar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
     uint8_t *dfl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
     if (n_ops) {
-      TNS_HIP(hipMemcpyAsync(dar, addr, 8 * n_ops, hipMemcpyHostToDevice, st));
-      TNS_HIP(hipMemcpyAsync(dfl, is_write, n_ops, hipMemcpyHostToDevice, st));
+      up_a = upload.add(dar, addr, 8 * n_ops);
+      up_f = upload.add(dfl, is_write, n_ops);
+      up_v = upload.add(V, value, sizeof(Fr) * n_ops);
+      upload.start();
     }
     ar = dar;
     fl = dfl;
+  } else if (n_ops && !v_in_place) {
+    TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   }
-  // host values (32 B an op, 4x the addresses): copied on the copy stream from a helper thread
-  // while the address commitment runs (commit_evals_pair: the value MSM is `late`)
-  const bool v_late = kind == hipMemcpyHostToDevice && n_ops > 0;
-  if (v_late) upload.start(c, V, value, sizeof(Fr) * n_ops);
-  else if (n_ops && !v_in_place) TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
   // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
   // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
@@ -962,6 +936,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   const bool flag_bytes = sumcheck_folds_take_flag_bytes(nv - lr);
   if (!flag_bytes) {
     O = (Fr *)d_o.ensure(sizeof(Fr) * L);
+    if (up_f >= 0) upload.wait(up_f, st);
     hipEvent_t in_ready;
     TNS_HIP(hipEventCreateWithFlags(&in_ready, hipEventDisableTiming));
     TNS_HIP(hipEventRecord(in_ready, st));
@@ -977,7 +952,10 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   // the commitment's sort reads the raw u64 addresses (8 bytes a scalar, no canonical copy)
   unsigned *a_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
   ScalarSource src_a;
-  src_a.prep = [=](hipStream_t s) { u64_tables_dev(s, ar, n_ops, L, A, nullptr, a_bits); };
+  src_a.prep = [=, &upload](hipStream_t s) {
+    if (up_a >= 0) upload.wait(up_a, s);
+    u64_tables_dev(s, ar, n_ops, L, A, nullptr, a_bits);
+  };
   src_a.canon_bits = a_bits;
   src_a.u64 = ar;
   src_a.n_u64 = n_ops;
@@ -997,11 +975,11 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   G1Affine cm[2];
   ScalarSource src_v;
   if (v_late) {
-    src_v.prep = [&upload](hipStream_t s) { upload.wait(s); };
+    src_v.prep = [&upload, up_v](hipStream_t s) { upload.wait(up_v, s); };
     src_v.late = true;
   }
   commit_evals_pair(c, srs->s, pa, pv, m, cm, &src_a, v_late ? &src_v : nullptr);
-  upload.wait(st);  // (done already unless a path above skipped the value MSM's prep)
+  if (up_v >= 0) upload.wait_all(st);  // everything below on st / side reads the uploaded inputs
   const G1Affine Ca = cm[0], Cv = cm[1];
   store_proj(Ca, out->commitments[0]);
   store_proj(Cv, out->commitments[1]);
@@ -1071,27 +1049,30 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   for (int i = 0; i < 6; i++) tm[i] = 0;
   TNS_HIP(hipStreamSynchronize(c->side));  // a failed earlier proof's folds may still read the tables
   SideDrain drain{c};
-  HostUpload upload;  // host table entries: uploaded under the index commitment
+  HostUpload upload(c);  // host inputs: lookup indices, then the table (under the index commitment)
   Timer t_h2d;
   DevBuf &d_idx_raw = c->prove_ws[0], &d_bad = c->prove_ws[1], &d_t = c->prove_ws[2], &d_i = c->prove_ws[3],
          &d_ct = c->prove_ws[5], &d_ci = c->prove_ws[6], &d_s = c->prove_ws[7];
   Fr *TB = (Fr *)d_t.ensure(sizeof(Fr) * LT), *I = (Fr *)d_i.ensure(sizeof(Fr) * LM);
   if (LT > n_entries) fr_fill_zero_dev(c, TB + n_entries, LT - n_entries);  // the padding (src/shout.rs:105-107)
   const bool t_late = kind == hipMemcpyHostToDevice && n_entries > 0;
-  if (t_late) {
-    upload.start(c, TB, entries, sizeof(Fr) * n_entries);
+  int up_i = -1, up_t = -1;
+  const uint64_t *ir = indices;
+  if (kind == hipMemcpyHostToDevice) {
+    if (n_lookups) {
+      uint64_t *dir = (uint64_t *)d_idx_raw.ensure(8 * n_lookups);
+      up_i = upload.add(dir, indices, 8 * n_lookups);
+      ir = dir;
+    }
+    if (t_late) up_t = upload.add(TB, entries, sizeof(Fr) * n_entries);
+    upload.start();
   } else if (n_entries) {
     TNS_HIP(hipMemcpyAsync(TB, entries, sizeof(Fr) * n_entries, kind, st));
   }
   // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
   unsigned hbad = 0;
-  const uint64_t *ir = indices;
   if (n_lookups) {
-    if (kind == hipMemcpyHostToDevice) {
-      uint64_t *dir = (uint64_t *)d_idx_raw.ensure(8 * n_lookups);
-      TNS_HIP(hipMemcpyAsync(dir, indices, 8 * n_lookups, hipMemcpyHostToDevice, st));
-      ir = dir;
-    }
+    if (up_i >= 0) upload.wait(up_i, st);
     unsigned *bad = (unsigned *)d_bad.ensure(sizeof(unsigned));
     TNS_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
     k_max_index_check<<<grid_for(n_lookups, 256), 256, 0, st>>>(ir, n_lookups, n_entries_total, bad);
@@ -1131,11 +1112,11 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   G1Affine cm[2];
   ScalarSource src_t;
   if (t_late) {
-    src_t.prep = [&upload](hipStream_t s) { upload.wait(s); };
+    src_t.prep = [&upload, up_t](hipStream_t s) { upload.wait(up_t, s); };
     src_t.late = true;
   }
   commit_evals_pair(c, srs->s, pt, pi, m, cm, t_late ? &src_t : nullptr, &src_i);  // (src/shout.rs:125-133)
-  upload.wait(st);
+  if (up_t >= 0) upload.wait_all(st);
   const G1Affine Ct = cm[0], Ci = cm[1];
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);

@@ -9,9 +9,11 @@
 #include <cstdio>
 #include <functional>
 #include <map>
+#include <condition_variable>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <vector>
 
@@ -246,7 +248,8 @@ struct Ctx {
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
   hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)
-  hipEvent_t copied = nullptr;
+  PinnedBuf stage;             // their pinned staging ring (upload.cpp, built on first use)
+  hipEvent_t stage_ev[16] = {};
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
@@ -279,6 +282,38 @@ struct Ctx {
   KernelProfiler prof;
   ~Ctx();
 };
+// upload.cpp: host-to-device copies of the drop-in provers' inputs, in add() order on the
+// context's copy stream from a helper thread (pinned staging ring, worker threads); wait(i, s)
+// makes stream s wait for item i.  The destructor joins the thread and drains the copy stream.
+class HostUpload {
+ public:
+  explicit HostUpload(Ctx *c);
+  ~HostUpload();
+  HostUpload(const HostUpload &) = delete;
+  HostUpload &operator=(const HostUpload &) = delete;
+  int add(void *dst, const void *src, size_t bytes);
+  void start();
+  void wait(int item, hipStream_t s);
+  void wait_all(hipStream_t s);
+
+ private:
+  struct Item {
+    void *dst = nullptr;
+    const void *src = nullptr;
+    size_t bytes = 0;
+    hipEvent_t ev = nullptr;
+  };
+  void run();
+  Ctx *c_;
+  std::vector<Item> items_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int queued_ = 0;
+  bool done_ = false;
+  hipError_t err_ = hipSuccess;
+};
+
 #define TNS_CAT2(a, b) a##b
 #define TNS_CAT(a, b) TNS_CAT2(a, b)
 // TNS_PROF(ctx, "stage", algorithmic_bytes_of_this_launch)
