@@ -412,19 +412,44 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
   for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) counts[cb + (size_t)d * Ts + k] = h[d];
 }
 
+// Packed tail of the sort (BucketSortJob::pk): after the second-to-last pass an entry needs only
+// the last pass's L key bits, its sign and its point index i (ibits bits), so that pass writes
+// them as one word  x = key_low << (ibits + 1) | sign << ibits | i  (4 bytes instead of a key and
+// a value), the last pass bins x by its top bits and writes the accumulation's value alone
+// (w stride + i | sign << 31; w = the key's window bits): 4 bytes fewer per entry written by the
+// second-to-last pass and read by the last.  Used when the usual split leaves room (n <= 2^22).
+// Independently, the last pass of every multi-pass sort writes the values only (PK 3): the
+// accumulation finds its runs from the bucket starts instead of a key per entry.
+struct PackArgs {
+  int ibits, L, wb, shared;
+  uint32_t stride;
+};
+
+// PK 0: keys + values in and out; 1: keys + values in, packed words out (okeys);
+// 2: packed words in (keys), values out (ovals); 3: keys + values in, values out
+__device__ __forceinline__ uint32_t pack_entry(const PackArgs &P, uint32_t key, uint32_t v) {
+  const uint32_t i = P.shared ? (v & 0x7fffffffu) - (key & ((1u << P.wb) - 1)) * P.stride : (v & 0x7fffffffu);
+  return ((key & ((1u << P.L) - 1)) << (P.ibits + 1)) | ((v >> 31) << P.ibits) | i;
+}
+__device__ __forceinline__ uint32_t unpack_value(const PackArgs &P, uint32_t x) {
+  const uint32_t i = x & ((1u << P.ibits) - 1), sign = (x >> P.ibits) & 1u;
+  const uint32_t w = P.shared ? (x >> (P.ibits + 1)) & ((1u << P.wb) - 1) : 0u;
+  return (w * P.stride + i) | (sign << 31);
+}
+
 // passes >= 2, scatter: tile -> LDS ordered by bin -> coalesced runs.  Segment s's block of
 // the scanned counts starts at offs[nbins tb]; one-tile segments (the common case in the last
 // pass) have zero counts there and take their bin offsets, and the next pass's segment
 // starts, from their own LDS scan.
-template <int TILE>
+template <int TILE, int PK>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, const uint32_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ vals,
                                                          uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
-                                                         uint32_t *__restrict__ nseg) {
+                                                         uint32_t *__restrict__ nseg, PackArgs P) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   constexpr int IPT = TILE / BS_BLOCK;
-  __shared__ uint32_t lk[TILE], lv[TILE];
+  __shared__ uint32_t lk[TILE], lv[PK == 2 ? 1 : TILE];
   const size_t g = blockIdx.x;
   if (g >= (G.ident ? S : G.tbase[S])) return;
   uint32_t s, tb, Ts;
@@ -445,7 +470,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     const int q = threadIdx.x + j * BS_BLOCK;
     if (q < m) {
       kk[j] = keys[a + q];
-      vv[j] = vals[a + q];
+      if (PK != 2) vv[j] = vals[a + q];
     }
   }
   __syncthreads();
@@ -464,11 +489,25 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     if ((int)threadIdx.x + j * BS_BLOCK < m) {
       const uint32_t slot = lbase[(kk[j] >> G.shift) & G.mask] + rk[j];
       lk[slot] = kk[j];
-      lv[slot] = vv[j];
+      if (PK != 2) lv[slot] = vv[j];
     }
   }
   __syncthreads();
-  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return (key >> G.shift) & G.mask; }, okeys, ovals);
+  for (int slot = threadIdx.x; slot < m; slot += BS_BLOCK) {  // coalesced runs (write_tile)
+    const uint32_t key = lk[slot];
+    const uint32_t d = (key >> G.shift) & G.mask;
+    const uint32_t pos = goff[d] + (uint32_t)slot - lbase[d];
+    if (PK == 0) {
+      okeys[pos] = key;
+      ovals[pos] = lv[slot];
+    } else if (PK == 3) {
+      ovals[pos] = lv[slot];
+    } else if (PK == 1) {
+      okeys[pos] = pack_entry(P, key, lv[slot]);
+    } else {
+      ovals[pos] = unpack_value(P, key);
+    }
+  }
 }
 
 // new segments s * nbins + d: their starts; nseg[S * nbins] = end of the last segment
@@ -563,6 +602,17 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   // remaining bits evenly (25-bit keys: 8, 8, 9 -- pass 2 with 256 instead of 512 bins writes
   // 128-byte runs: 1.21 -> 1.02 ms at 2^24)
   bits[npass - 1] = std::min(keybits, BS_MAXBITS);
+  // packed tail: the last pass keeps L <= 31 - ibits key bits so that its input fits one word
+  // (2^24 points: 7; 25-bit keys then split 9, 9, 7); TNS_BS_PACK=0 keeps keys + values (A/B)
+  int ibits = 1;
+  while (((size_t)1 << ibits) < n) ibits++;
+  // (a 7-bit last pass for 2^24 points measured slower: 9, 9, 7 moved the cost into 512-bin
+  // passes, +3.3 ms of sort per C4 step against -0.8 ms of reads; so only when the usual split
+  // leaves room: n <= 2^22 with a 9-bit last pass).  Values-only last pass (vo): whenever there
+  // is more than one pass -- the accumulation reads no keys (C4: k_accumulate 9.10 -> 8.8 ms).
+  const char *pke = getenv("TNS_BS_PACK"), *voe = getenv("TNS_BS_VO");
+  J.vo = npass >= 2 && !(voe && voe[0] == '0');
+  J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32;
   for (int p = 0, rest = keybits - bits[npass - 1]; p < npass - 1; p++) {
     bits[p] = (rest + (npass - 2 - p)) / (npass - 1 - p);
     rest -= bits[p];
@@ -579,7 +629,11 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
     for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= BS_MAXBITS;
     if (ok)
       for (int p = 0; p < npass; p++) bits[p] = v[p];
+    if (ok) J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32;
   }
+  J.ibits = ibits;
+  J.shared = shared;
+  J.stride = stride;
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
@@ -631,6 +685,7 @@ void bucket_sort_passes(BucketSortJob &J) {
   const size_t E = J.E;
   uint32_t **seg = J.seg;
   for (int p = 1; p < npass; p++) {
+    J.p = p;
     J.nb = 1 << bits[p];
     J.shift -= bits[p];
     int tile = pass_tile(p);
@@ -681,7 +736,10 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
     k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(J.tbase, S, J.desc);
     TNS_LAUNCH_CHECK();
   }
-  PassGeom G{J.seg[cur], J.tbase, J.desc, J.shift, nb, (uint32_t)nb - 1, ident, mb};
+  // packed tail: pass npass - 2 writes packed words, the last pass bins them by their top bits
+  const int pk = J.pk ? (J.p == J.npass - 2 ? 1 : J.p == J.npass - 1 ? 2 : 0) : J.vo && J.p == J.npass - 1 ? 3 : 0;
+  const PackArgs PA{J.ibits, J.bits[J.npass - 1], J.wb, J.shared ? 1 : 0, J.stride};
+  PassGeom G{J.seg[cur], J.tbase, J.desc, pk == 2 ? J.ibits + 1 : J.shift, nb, (uint32_t)nb - 1, ident, mb};
   uint32_t *counts = J.counts, *offs = J.offs;
   if (!ident) {
     if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
@@ -690,12 +748,18 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
   }
-  if (tile == 4096)
-    k_bs_scatter<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, J.K[cur], J.V[cur], J.K[cur ^ 1],
-                                                                   J.V[cur ^ 1], J.seg[cur ^ 1]);
-  else
-    k_bs_scatter<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, J.K[cur], J.V[cur], J.K[cur ^ 1],
-                                                                      J.V[cur ^ 1], J.seg[cur ^ 1]);
+  {
+    auto *kern = tile == 4096 ? (pk == 0   ? k_bs_scatter<4096, 0>
+                                 : pk == 1 ? k_bs_scatter<4096, 1>
+                                 : pk == 2 ? k_bs_scatter<4096, 2>
+                                           : k_bs_scatter<4096, 3>)
+                              : (pk == 0   ? k_bs_scatter<BS_TILE, 0>
+                                 : pk == 1 ? k_bs_scatter<BS_TILE, 1>
+                                 : pk == 2 ? k_bs_scatter<BS_TILE, 2>
+                                           : k_bs_scatter<BS_TILE, 3>);
+    kern<<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, offs, J.K[cur], J.V[cur], J.K[cur ^ 1], J.V[cur ^ 1],
+                                                     J.seg[cur ^ 1], PA);
+  }
   TNS_LAUNCH_CHECK();
   k_bs_segs<<<grid_for(S * nb + 1, 256), 256, 0, st>>>(G, S, offs, J.seg[cur ^ 1]);
   TNS_LAUNCH_CHECK();
@@ -719,7 +783,7 @@ BucketOrder bucket_sort_finish(BucketSortJob &J) {
     k_bs_bucket_starts<<<grid_for(nbk + 1, 256), 256, 0, ln.stream>>>(J.seg[J.cur], nbk, J.wb, bstart);
     TNS_LAUNCH_CHECK();
   }
-  return BucketOrder{J.K[J.cur], J.V[J.cur], bstart, J.wb, entries};
+  return BucketOrder{J.vo ? nullptr : J.K[J.cur], J.V[J.cur], bstart, J.wb, entries};
 }
 
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,

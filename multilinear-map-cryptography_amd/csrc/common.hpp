@@ -447,7 +447,7 @@ struct ScalarSource {
 void msm_pair_dev(Ctx *c, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]);
 // bucket_sort.hip: the MSM's digit entries grouped by bucket (bucket k = [bstart[k], bstart[k+1]))
 struct BucketOrder {
-  uint32_t *keys, *vals, *bstart;
+  uint32_t *keys, *vals, *bstart;  // keys == nullptr: packed tail, the runs come from bstart alone
   int ks;          // bucket = key >> ks
   size_t entries;  // sorted entries (non-zero digits) when read back, else SIZE_MAX
 };
@@ -473,6 +473,12 @@ struct BucketSortJob {
   uint32_t *counts = nullptr, *offs = nullptr, *tcount = nullptr, *tbase = nullptr, *desc = nullptr;
   uint32_t *mcount = nullptr, *mbase = nullptr;
   uint32_t *valid = nullptr;  // device: the entry count
+  // packed tail (pk): the second-to-last pass writes one u32 per entry -- the last pass's key
+  // bits, the sign and the point index i (ibits bits) -- and the last pass reads that word and
+  // writes the accumulation's values only (no keys: runs come from the bucket starts)
+  bool pk = false, vo = false, shared = false;  // vo: the last pass writes values only
+  int ibits = 0, p = 0;
+  uint32_t stride = 0;
 };
 void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J);

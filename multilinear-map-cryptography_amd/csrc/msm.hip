@@ -198,37 +198,69 @@ struct HeadTail {
   G1Xyzz head, tail;
 };
 
+// the bucket holding sorted entry p < valid: the largest k with bstart[k] <= p (bstart is
+// non-decreasing, bstart[0] = 0, bstart[nb] = valid; empty buckets repeat their successor's start)
+__device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ bstart, size_t nb, size_t p) {
+  size_t lo = 0, hi = nb;
+  while (hi - lo > 1) {
+    const size_t mid = (lo + hi) >> 1;
+    if (bstart[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return (uint32_t)lo;
+}
+
+// keys == nullptr (packed sort tail): a chunk finds its first bucket by a binary search of the
+// bucket starts and every later run boundary from the next start -- no key per entry.
 __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals,
                                                     const uint32_t *__restrict__ valid_p,
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
                                                     HeadTail *__restrict__ ht, size_t nchunks, int ks,
-                                                    int acc_k) {
+                                                    int acc_k, const uint32_t *__restrict__ bstart, size_t nb) {
   const size_t valid = *valid_p;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
     const size_t a = t * acc_k;
     if (a >= valid) continue;
     const size_t b = a + acc_k < valid ? a + acc_k : valid;
-    uint32_t cur = keys[a] >> ks;
     // a run is a head (it began before this chunk) iff it is the chunk's first run and entry
     // a - 1 has its bucket, a tail (it goes on after the chunk) iff it is the last run and entry
     // b has its bucket: two key loads per chunk instead of the run's bounds at every flush.
     // Flushed sums stay in the lazy domain [0, 2M): the fixup and the reduction add them lazily.
-    const bool head_run = a > 0 && (keys[a - 1] >> ks) == cur;
-    const uint32_t after = b < valid ? keys[b] >> ks : 0xffffffffu;
+    uint32_t cur, after;
+    bool head_run;
+    size_t nxt = 0;  // (no keys) the start of the bucket after `cur`
+    if (keys) {
+      cur = keys[a] >> ks;
+      head_run = a > 0 && (keys[a - 1] >> ks) == cur;
+      after = b < valid ? keys[b] >> ks : 0xffffffffu;
+    } else {
+      cur = bucket_of(bstart, nb, a);
+      head_run = bstart[cur] < a;
+      nxt = bstart[cur + 1];
+      after = 0xffffffffu;
+    }
     bool first = true;
     G1Xyzz acc = G1Xyzz::inf();
     for (size_t p = a;; p++) {
-      const uint32_t k = (p < b) ? keys[p] >> ks : 0xffffffffu;
-      if (k != cur) {  // flush the run of bucket `cur`
+      const bool brk = keys ? p >= b || (keys[p] >> ks) != cur : p >= b || p >= nxt;
+      if (brk) {  // flush the run of bucket `cur`
+        const bool tail = keys ? after == cur : nxt > b;
         if (first && head_run) ht[t].head = acc;
-        else if (p >= b && after == cur) ht[t].tail = acc;
+        else if (p >= b && tail) ht[t].tail = acc;
         else buckets[cur] = acc;
         if (p >= b) break;
         first = false;
-        cur = k;
+        if (keys) {
+          cur = keys[p] >> ks;
+        } else {
+          do {  // skip empty buckets
+            cur++;
+            nxt = bstart[cur + 1];
+          } while (nxt <= p);
+        }
         acc = G1Xyzz::inf();
       }
       // (gathering entry p + 1 ahead of this addition measured no faster: 39.48 vs 39.46 ms of
@@ -264,7 +296,7 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ valid_p,
                                                    const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
                                                    int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks,
-                                                   int acc_k) {
+                                                   int acc_k, const uint32_t *__restrict__ bstart, size_t nb) {
   const size_t valid = *valid_p;
   const int j = threadIdx.x & (FIX_FAN - 1);
   const size_t stride = (size_t)gridDim.x * blockDim.x / FIX_FAN;
@@ -273,7 +305,8 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
     size_t span = (size_t)acc_k;
     for (int l = 0; l < level; l++) span *= FIX_FAN;
     const size_t a = g * span, b = a + span;  // entries covered
-    const bool uniform = b <= valid && (keys[a] >> ks) == (keys[b - 1] >> ks);
+    const bool uniform = b <= valid && (keys ? (keys[a] >> ks) == (keys[b - 1] >> ks)
+                                             : bstart[bucket_of(bstart, nb, a) + 1] >= b);
     G1Xyzz acc = G1Xyzz::inf();
     if (uniform) acc = level == 1 ? ht[g * FIX_FAN + j].head : below[g * FIX_FAN + j];
     for (int off = FIX_FAN / 2; off > 0; off >>= 1) {  // every lane of the wave takes part
@@ -817,7 +850,7 @@ static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * J.n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
     k_accumulate<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets,
-                                                                     ht, J.nchunks, J.ks, J.acc_k);
+                                                                     ht, J.nchunks, J.ks, J.acc_k, J.bstart, J.P.nb);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
@@ -851,7 +884,8 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
         F.lv[l] = base + o;
         o += F.len[l];
         k_fix_level<<<grid_for(F.len[l] * FIX_FAN, 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l,
-                                                                                  F.len[l], F.lv[l], ks, acc_k);
+                                                                                  F.len[l], F.lv[l], ks, acc_k,
+                                                                                  bstart, P.nb);
         TNS_LAUNCH_CHECK();
       }
     }

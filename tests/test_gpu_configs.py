@@ -155,3 +155,16 @@ def test_twist_msm_sort_variant_same_proof():
         ctx.set_msm_sort(False)
     assert a == b
     assert s_cub == ts.Shout(pp).prove_arrays(entries, idx)
+
+
+@pytest.mark.parametrize("var", ["TNS_BS_PACK", "TNS_BS_VO"])
+@pytest.mark.parametrize("L", [14, 18])
+def test_twist_packed_sort_tail_same_proof(L, var, monkeypatch):
+    """The packed sort tail (the last pass reads one word per entry and writes values only; the
+    accumulation finds its runs from the bucket starts) gives the proof of the key + value sort."""
+    pp, _ = params(L)
+    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
+    a = ts.Twist(pp).prove_soa(addr, val, isw)
+    monkeypatch.setenv(var, "0")
+    b = ts.Twist(pp).prove_soa(addr, val, isw)
+    assert a == b
