@@ -486,6 +486,24 @@ __device__ __forceinline__ bool fq_zero_lazy(const Fq &a) {
   return z == 0 || m == 0;
 }
 
+// K - a for a constant K >= a (no borrow out, no correction): K = M negates a canonical value,
+// K = 2M forms the lazy-domain negation of a value in [0, 2M).  a is tied to the result (no
+// early-clobber operand, see field_asm.inc); the borrow-chain limbs of K come from VGPRs (one
+// constant-bus read per VALU instruction on gfx9: VCC is already one).
+template <class C, bool TWO_M>
+__device__ __forceinline__ Fp<C> const_minus_dev(const Fp<C> &a) {
+  Fp<C> r = a;
+  const u32 *K = TWO_M ? C::M2 : C::M;
+  asm("v_sub_co_u32_e32 %0, vcc, %8, %0\n\tv_subb_co_u32_e32 %1, vcc, %9, %1, vcc\n\t"
+      "v_subb_co_u32_e32 %2, vcc, %10, %2, vcc\n\tv_subb_co_u32_e32 %3, vcc, %11, %3, vcc\n\t"
+      "v_subb_co_u32_e32 %4, vcc, %12, %4, vcc\n\tv_subb_co_u32_e32 %5, vcc, %13, %5, vcc\n\t"
+      "v_subb_co_u32_e32 %6, vcc, %14, %6, vcc\n\tv_subb_co_u32_e32 %7, vcc, %15, %7, vcc"
+      : "+v"(r.v[0]), "+v"(r.v[1]), "+v"(r.v[2]), "+v"(r.v[3]), "+v"(r.v[4]), "+v"(r.v[5]), "+v"(r.v[6]), "+v"(r.v[7])
+      : "s"(K[0]), "v"(K[1]), "v"(K[2]), "v"(K[3]), "v"(K[4]), "v"(K[5]), "v"(K[6]), "v"(K[7])
+      : "vcc");
+  return r;
+}
+
 __device__ __forceinline__ G1Xyzz xyzz_madd_lazy(const G1Xyzz &p, const G1Affine &q) {
   if (q.is_inf()) return p;
   if (p.is_inf()) {
@@ -504,15 +522,17 @@ __device__ __forceinline__ G1Xyzz xyzz_madd_lazy(const G1Xyzz &p, const G1Affine
     if (fq_zero_lazy(R)) return xyzz_mdbl(q);
     return G1Xyzz::inf();
   }
+  // ordered for register pressure: ZZ1, ZZZ1 die in ZZ3 / ZZZ3 right after PP / PPP, X1 and PP
+  // in Q; the peak live set is PP, PPP, R, X1, Y1 and the two Z coordinates
   const Fq PP = sqr_lazy_dev(P);
   const Fq PPP = mul_lazy_dev(P, PP);
-  const Fq Q = mul_lazy_dev(p.x, PP);
   G1Xyzz r;
-  r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
-  // Y3 = R (Q - X3) - Y1 PPP as ONE reduction of R (Q - X3) + Y1 (2M - PPP)
-  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), p.y, sub2_dev(Fq::zero(), PPP));
   r.zz = mul_lazy_dev(p.zz, PP);
   r.zzz = mul_lazy_dev(p.zzz, PPP);
+  const Fq Q = mul_lazy_dev(p.x, PP);
+  r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
+  // Y3 = R (Q - X3) - Y1 PPP as ONE reduction of R (Q - X3) + Y1 (2M - PPP)  (PPP in [0, 2M))
+  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), p.y, const_minus_dev<FqCfg, true>(PPP));
   return r;
 }
 
@@ -545,7 +565,7 @@ __device__ __forceinline__ G1Xyzz xyzz_add_lazy(const G1Xyzz &p, const G1Xyzz &q
   const Fq Q = mul_lazy_dev(U1, PP);
   G1Xyzz r;
   r.x = sub2_dev(sub2_dev(sqr_lazy_dev(R), PPP), add2_dev(Q, Q));
-  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), S1, sub2_dev(Fq::zero(), PPP));  // one reduction
+  r.y = mul2_lazy_dev(R, sub2_dev(Q, r.x), S1, const_minus_dev<FqCfg, true>(PPP));  // one reduction
   r.zz = mul_lazy_dev(mul_lazy_dev(p.zz, q.zz), PP);
   r.zzz = mul_lazy_dev(mul_lazy_dev(p.zzz, q.zzz), PPP);
   return r;

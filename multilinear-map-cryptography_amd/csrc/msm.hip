@@ -179,6 +179,12 @@ __global__ void __launch_bounds__(256) k_bucket_bounds(const uint32_t *__restric
 #define TNS_ACC_PTMASK 0x7fffffffu
 #endif
 
+// TNS_ACC_PREFETCH=1 (A/B build): software-pipelined gathers -- entry p + 1's point and entry
+// p + 2's value are loaded while entry p is added
+#ifndef TNS_ACC_PREFETCH
+#define TNS_ACC_PREFETCH 0
+#endif
+
 // the accumulation's point gather (TNS_ACC_NT=1 A/B build: non-temporal loads)
 typedef uint32_t acc_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ G1Affine load_point(const G1Affine *__restrict__ pts, uint32_t i) {
@@ -212,7 +218,11 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ bstar
 
 // keys == nullptr (packed sort tail): a chunk finds its first bucket by a binary search of the
 // bucket starts and every later run boundary from the next start -- no key per entry.
-__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ keys,
+// TNS_ACC_MINB (A/B builds): __launch_bounds__ minimum blocks per CU (4: 128 VGPRs, 4 waves/SIMD)
+#ifndef TNS_ACC_MINB
+#define TNS_ACC_MINB 1
+#endif
+__global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals,
                                                     const uint32_t *__restrict__ valid_p,
                                                     const G1Affine *__restrict__ pts,
@@ -244,6 +254,10 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
     }
     bool first = true;
     G1Xyzz acc = G1Xyzz::inf();
+#if TNS_ACC_PREFETCH
+    uint32_t v1 = vals[a], v2 = a + 1 < b ? vals[a + 1] : 0u;
+    G1Affine q1 = load_point(pts, v1 & TNS_ACC_PTMASK);
+#endif
     for (size_t p = a;; p++) {
       const bool brk = keys ? p >= b || (keys[p] >> ks) != cur : p >= b || p >= nxt;
       if (brk) {  // flush the run of bucket `cur`
@@ -265,11 +279,23 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
       }
       // (gathering entry p + 1 ahead of this addition measured no faster: 39.48 vs 39.46 ms of
       // accumulation per C4 step -- three waves per SIMD hide the gather)
+#if TNS_ACC_PREFETCH
+      const uint32_t v = v1;
+      G1Affine q = q1;
+      if (p + 1 < b) {  // entry p + 1's point (its value arrived an iteration ago), entry p + 2's value
+        q1 = load_point(pts, v2 & TNS_ACC_PTMASK);
+        v1 = v2;
+        if (p + 2 < b) v2 = vals[p + 2];
+      }
+#else
       const uint32_t v = vals[p];
       G1Affine q = load_point(pts, v & TNS_ACC_PTMASK);
-      const Fq ny = sub_dev(Fq::zero(), q.y);  // -y (0 stays 0: the identity is (0, 0))
+#endif
+      // -y = M - y (y canonical); the identity (0, 0) keeps y = 0
+      const Fq ny = const_minus_dev<FqCfg, false>(q.y);
+      const bool negy = (v >> 31) && !q.y.is_zero();
 #pragma unroll
-      for (int l = 0; l < 8; l++) q.y.v[l] = (v >> 31) ? ny.v[l] : q.y.v[l];
+      for (int l = 0; l < 8; l++) q.y.v[l] = negy ? ny.v[l] : q.y.v[l];
       acc = xyzz_madd_lazy(acc, q);
     }
   }
