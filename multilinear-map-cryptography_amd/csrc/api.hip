@@ -221,6 +221,9 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
     if (s) {
       a.prep = s->prep;
       a.late = s->late;
+      a.chunks = s->chunks;
+      a.chunk_len = s->chunk_len;
+      a.chunk_prep = s->chunk_prep;
       a.canon = s->canon;
       a.canon_bits = s->canon_bits;
       a.u64 = s->u64;
@@ -866,6 +869,13 @@ __global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, ui
 // On every exit of a prove call (an exception included): nothing this call queued on the side
 // stream (the flag table, the zero-closure folds: they read the caller's value / is_write
 // buffers in the device-resident entry points) is still running when the call returns.
+// node ranges the drop-in provers upload (and commit) the late vector in (TNS_UPLOAD_CHUNKS)
+static int upload_chunks() {
+  const char *e = getenv("TNS_UPLOAD_CHUNKS");
+  const int k = e ? atoi(e) : 4;
+  return std::max(1, std::min(64, k));
+}
+
 struct SideDrain {
   Ctx *c;
   ~SideDrain() { (void)hipStreamSynchronize(c->side); }
@@ -914,13 +924,22 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   // is `late` in commit_evals_pair and waits for it
   const bool v_late = kind == hipMemcpyHostToDevice && n_ops > 0;
   int up_a = -1, up_f = -1, up_v = -1;
+  // the values arrive in v_chunks node ranges, each committed as it lands (TNS_UPLOAD_CHUNKS,
+  // default 4; 1 = one upload, one MSM after it); padded slices (L > n_ops) keep one MSM
+  int v_chunks = v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? upload_chunks() : 1;
+  const size_t v_per = (n_ops + v_chunks - 1) / std::max(v_chunks, 1);
+  if (v_per) v_chunks = (int)((n_ops + v_per - 1) / v_per);  // chunks actually formed
   if (kind == hipMemcpyHostToDevice) {
     uint64_t *dar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
     uint8_t *dfl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
     if (n_ops) {
       up_a = upload.add(dar, addr, 8 * n_ops);
       up_f = upload.add(dfl, is_write, n_ops);
-      up_v = upload.add(V, value, sizeof(Fr) * n_ops);
+      for (int k = 0; k < v_chunks; k++) {  // item ids up_v, up_v + 1, ...
+        const int id = upload.add(V + (size_t)k * v_per, value + 4 * (size_t)k * v_per,
+                                  sizeof(Fr) * std::min(v_per, n_ops - (size_t)k * v_per));
+        if (k == 0) up_v = id;
+      }
       upload.start();
     }
     ar = dar;
@@ -975,8 +994,15 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   G1Affine cm[2];
   ScalarSource src_v;
   if (v_late) {
-    src_v.prep = [&upload, up_v](hipStream_t s) { upload.wait(up_v, s); };
+    src_v.prep = [&upload, up_v, v_chunks](hipStream_t s) {
+      for (int k = 0; k < v_chunks; k++) upload.wait(up_v + k, s);
+    };
     src_v.late = true;
+    if (v_chunks > 1 && m.size == 1) {
+      src_v.chunks = v_chunks;
+      src_v.chunk_len = v_per;
+      src_v.chunk_prep = [&upload, up_v](int k, hipStream_t s) { upload.wait(up_v + k, s); };
+    }
   }
   commit_evals_pair(c, srs->s, pa, pv, m, cm, &src_a, v_late ? &src_v : nullptr);
   if (up_v >= 0) upload.wait_all(st);  // everything below on st / side reads the uploaded inputs

@@ -433,11 +433,21 @@ struct MsmArgs {
   // the scalars are still arriving (a host upload in flight; prep waits for it): msm_pair_dev
   // queues the other MSM whole before this one's prep
   bool late = false;
+  // late and chunks > 1: the scalars arrive in `chunks` equal node ranges (the last one ragged),
+  // chunk k ready once chunk_prep(k, stream) returns; msm_pair_dev sums one MSM per chunk as
+  // each lands (table plans use the window table at the chunk's offset), so only the last
+  // chunk's MSM follows the upload
+  int chunks = 0;
+  size_t chunk_len = 0;  // chunk k = scalars [k chunk_len, min(n, (k + 1) chunk_len))
+  std::function<void(int, hipStream_t)> chunk_prep;
 };
 // how one vector of commit_evals_pair gets ready (the MsmArgs fields of the same names)
 struct ScalarSource {
   std::function<void(hipStream_t)> prep;
   bool late = false;
+  int chunks = 0;                                   // (MsmArgs::chunks, chunk_len, chunk_prep)
+  size_t chunk_len = 0;
+  std::function<void(int, hipStream_t)> chunk_prep;
   const Fr *canon = nullptr;
   const unsigned *canon_bits = nullptr;
   const uint64_t *u64 = nullptr;

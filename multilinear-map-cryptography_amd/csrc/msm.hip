@@ -735,7 +735,7 @@ static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
 static void msm_finish_sort(MsmJob &J);
 static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const SortInput &in,
                             size_t n, const FixedBase *fb, unsigned bits, MsmJob &J, hipEvent_t sorted = nullptr,
-                            bool defer = false) {
+                            bool defer = false, size_t fb_off = 0) {
   J.lane = &ln;
   J.ctx = ctx;
   J.sorted_ev = sorted;
@@ -768,14 +768,14 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   P.c = best_window(n, (int)bits, 20, false, w1 && w1[0] == '0' ? 0 : 23);
   if (ctx->msm_c >= 4) P.c = ctx->msm_c;
   P.W = windows_for((int)bits, P.c);
-  if (fb && ctx->msm_tables && fb->n >= n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
+  if (fb && ctx->msm_tables && fb->n >= fb_off + n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
     const int Ws = windows_for((int)bits, fb->c);
     if (Ws <= fb->W && plan_cost(n, Ws, fb->c, 1) < plan_cost(n, P.W, P.c, P.W)) {
       P.shared = true;
       P.c = fb->c;
       P.W = Ws;
       P.stride = fb->n;
-      points = fb->table.as<G1Affine>();
+      points = fb->table.as<G1Affine>() + fb_off;  // T[w n + fb_off + i]: value w stride + i
     }
   }
   finish_plan(P);
@@ -1052,6 +1052,25 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     if (a.n > 64) ba = bits_result(l0);
     msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja);
     msm_launch_reduce(ctx, ja);
+    if (b.chunks > 1) {  // one MSM per uploaded chunk, each as soon as it lands
+      const size_t per = b.chunk_len;
+      G1Xyzz acc = G1Xyzz::inf();
+      for (int k = 0; k < b.chunks && (size_t)k * per < b.n; k++) {
+        const size_t off = (size_t)k * per, cnt = std::min(per, b.n - off);
+        MsmArgs bk{b.points + off, b.scalars + off, cnt, b.fb};
+        bk.prep = [&b, k](hipStream_t s) { b.chunk_prep(k, s); };
+        MsmJob jk;
+        unsigned bk_bits = 254;
+        const SortInput ck = start(l1, bk);
+        if (cnt > 64) bk_bits = bits_result(l1);
+        msm_launch_sort(ctx, l1, bk.points, bk.scalars, ck, cnt, b.fb, bk_bits, jk, nullptr, false, off);
+        msm_launch_reduce(ctx, jk);
+        acc = xyzz_add(acc, msm_complete(ctx, jk));  // the lane's host buffer serves the next chunk
+      }
+      out[0] = msm_complete(ctx, ja);
+      out[1] = acc;
+      return;
+    }
     cb = start(l1, b);
     if (b.n > 64) bb = bits_result(l1);
     msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb);

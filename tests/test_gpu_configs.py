@@ -168,3 +168,24 @@ def test_twist_packed_sort_tail_same_proof(L, var, monkeypatch):
     monkeypatch.setenv(var, "0")
     b = ts.Twist(pp).prove_soa(addr, val, isw)
     assert a == b
+
+
+@pytest.mark.parametrize("chunks", ["1", "3", "4", "7"])
+def test_twist_dropin_chunked_value_commitment(chunks, monkeypatch):
+    """The drop-in prover commits the value vector chunk by chunk as its upload lands
+    (TNS_UPLOAD_CHUNKS node ranges, one MSM each, summed): full-width values take the window-table
+    plan at each chunk's offset, the bench trace's narrow values the per-window plan; both equal
+    the device-resident proof (one MSM over the whole vector)."""
+    L = 16
+    pp, _ = params(L)
+    n = 1 << (L + 2)
+    addr, val, isw = ts.bench_trace(1 << L, n)
+    rng = np.random.default_rng(11)
+    wide = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+    wide[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
+    ctx = pp.commitment_params.srs.ctx
+    monkeypatch.setenv("TNS_UPLOAD_CHUNKS", chunks)
+    for v in (val, wide):
+        d = [ts.DeviceBuffer(ctx, x) for x in (addr, v, isw)]
+        want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
+        assert ts.Twist(pp).prove_soa(addr, v, isw) == want
