@@ -228,7 +228,8 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
                                                     HeadTail *__restrict__ ht, size_t nchunks, int ks,
-                                                    int acc_k, const uint32_t *__restrict__ bstart, size_t nb) {
+                                                    int acc_k, const uint32_t *__restrict__ bstart, size_t nb,
+                                                    uint2 *__restrict__ cbk) {
   const size_t valid = *valid_p;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
@@ -253,6 +254,7 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
       after = 0xffffffffu;
     }
     bool first = true;
+    const uint32_t first_bucket = cur;
     G1Xyzz acc = G1Xyzz::inf();
 #if TNS_ACC_PREFETCH
     uint32_t v1 = vals[a], v2 = a + 1 < b ? vals[a + 1] : 0u;
@@ -265,7 +267,10 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
         if (first && head_run) ht[t].head = acc;
         else if (p >= b && tail) ht[t].tail = acc;
         else buckets[cur] = acc;
-        if (p >= b) break;
+        if (p >= b) {
+          cbk[t] = make_uint2(first_bucket, cur);  // the buckets of entries a and b - 1 (k_fix_level)
+          break;
+        }
         first = false;
         if (keys) {
           cur = keys[p] >> ks;
@@ -322,7 +327,7 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
                                                    const uint32_t *__restrict__ valid_p,
                                                    const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
                                                    int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks,
-                                                   int acc_k, const uint32_t *__restrict__ bstart, size_t nb) {
+                                                   int acc_k, const uint2 *__restrict__ cbk) {
   const size_t valid = *valid_p;
   const int j = threadIdx.x & (FIX_FAN - 1);
   const size_t stride = (size_t)gridDim.x * blockDim.x / FIX_FAN;
@@ -331,8 +336,9 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
     size_t span = (size_t)acc_k;
     for (int l = 0; l < level; l++) span *= FIX_FAN;
     const size_t a = g * span, b = a + span;  // entries covered
-    const bool uniform = b <= valid && (keys ? (keys[a] >> ks) == (keys[b - 1] >> ks)
-                                             : bstart[bucket_of(bstart, nb, a) + 1] >= b);
+    // every entry of [a, b) in one bucket: the bucket of entry a (that chunk's first) is the bucket
+    // of entry b - 1 (the last chunk's last), as k_accumulate recorded them
+    const bool uniform = b <= valid && cbk[a / acc_k].x == cbk[(b - 1) / acc_k].y;
     G1Xyzz acc = G1Xyzz::inf();
     if (uniform) acc = level == 1 ? ht[g * FIX_FAN + j].head : below[g * FIX_FAN + j];
     for (int off = FIX_FAN / 2; off > 0; off >>= 1) {  // every lane of the wave takes part
@@ -875,8 +881,10 @@ static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
   {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * J.n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
+    uint2 *cbk = (uint2 *)ln.ws[16].ensure(sizeof(uint2) * J.nchunks);
     k_accumulate<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets,
-                                                                     ht, J.nchunks, J.ks, J.acc_k, J.bstart, J.P.nb);
+                                                                     ht, J.nchunks, J.ks, J.acc_k, J.bstart, J.P.nb,
+                                                                     cbk);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
@@ -911,7 +919,7 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
         o += F.len[l];
         k_fix_level<<<grid_for(F.len[l] * FIX_FAN, 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l,
                                                                                   F.len[l], F.lv[l], ks, acc_k,
-                                                                                  bstart, P.nb);
+                                                                                  (const uint2 *)ln.ws[16].p);
         TNS_LAUNCH_CHECK();
       }
     }
