@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -141,18 +142,60 @@ __device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out
 
 static_assert(BS_MAXBINS <= 2 * BS_BLOCK, "two bins per thread in the block scan");
 
+// Key formats between passes (BucketSortJob::kf): the keys a pass writes only need the key bits
+// the later passes still sort by.  KF_U32: 4-byte keys; KF_U16: 2-byte keys (<= 16 bits left);
+// KF_U16S: 17 bits left -- bits [1, 17) in 2 bytes, bit 0 in bit 30 of the value (values are
+// < 2^30 there, bit 31 is the sign).  The reader restores the key's low bits and the value.
+enum { KF_U32 = 0, KF_U16 = 1, KF_U16S = 2 };
+constexpr uint32_t BS_STASH = 0x40000000u;
+
+__device__ __forceinline__ void store_entry(int kf, uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
+                                            uint32_t pos, uint32_t key, uint32_t val) {
+  if (kf == KF_U32) {
+    okeys[pos] = key;
+    ovals[pos] = val;
+  } else if (kf == KF_U16) {
+    reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)key;
+    ovals[pos] = val;
+  } else {
+    reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)(key >> 1);
+    ovals[pos] = val | ((key & 1u) << 30);
+  }
+}
+
+// entry i's key (the low bits a pass still needs) and value in format kf
+__device__ __forceinline__ void load_entry(int kf, const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
+                                           size_t i, uint32_t &key, uint32_t &val) {
+  val = vals[i];
+  if (kf == KF_U32) {
+    key = keys[i];
+  } else {
+    key = reinterpret_cast<const uint16_t *>(keys)[i];
+    if (kf == KF_U16S) {
+      key = (key << 1) | ((val >> 30) & 1u);
+      val &= ~BS_STASH;
+    }
+  }
+}
+
+// key only (histograms; KF_U16S without its bit 0: only passes with shift >= 1 read that format)
+__device__ __forceinline__ uint32_t load_key(int kf, const uint32_t *__restrict__ keys, size_t i) {
+  if (kf == KF_U32) return keys[i];
+  const uint32_t k = reinterpret_cast<const uint16_t *>(keys)[i];
+  return kf == KF_U16 ? k : k << 1;
+}
+
 // Tile writer: entries already placed in lk/lv by bin (bin d at [lbase[d], lbase[d] + cnt));
 // consecutive lanes store consecutive slots of a bin's run at goff[d] + (slot - lbase[d]).
 template <class BinOf>
 __device__ __forceinline__ void write_tile(const uint32_t *lk, const uint32_t *lv, int m, const uint32_t *lbase,
-                                           const uint32_t *goff, BinOf bin, uint32_t *__restrict__ okeys,
+                                           const uint32_t *goff, BinOf bin, int kf, uint32_t *__restrict__ okeys,
                                            uint32_t *__restrict__ ovals) {
   for (int slot = threadIdx.x; slot < m; slot += BS_BLOCK) {
     const uint32_t key = lk[slot];
     const uint32_t d = bin(key);
     const uint32_t pos = goff[d] + (uint32_t)slot - lbase[d];
-    okeys[pos] = key;
-    ovals[pos] = lv[slot];
+    store_entry(kf, okeys, ovals, pos, key, lv[slot]);
   }
 }
 
@@ -172,7 +215,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1(DigitArgs A, int shift, 
 // pass 1 scatter: digits -> LDS ordered by bin -> coalesced runs
 template <int TILE>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift, int nbins, size_t T1,
-                                                          const uint32_t *__restrict__ offs,
+                                                          const uint32_t *__restrict__ offs, int kf,
                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   __shared__ uint32_t lk[TILE], lv[TILE];
@@ -194,7 +237,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift
   });
   __syncthreads();
   const int m = (int)h[nbins - 1];  // the last bin's cursor ends at the tile's entry count
-  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, keys, vals);
+  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, kf, keys, vals);
 }
 
 // ---- pass 1 with a compile-time window plan (C bits, W windows): the digit of window w sits
@@ -255,7 +298,7 @@ constexpr uint32_t BS_NOKEY = 0x40000000u;  // empty entry slot (keys are < 2^30
 
 template <int TILE, int C, int W, int SPT>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int shift, int nbins, size_t T1,
-                                                             const uint32_t *__restrict__ offs,
+                                                             const uint32_t *__restrict__ offs, int kf,
                                                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   __shared__ uint32_t lk[TILE], lv[TILE];
@@ -304,7 +347,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
     }
   }
   __syncthreads();
-  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, keys, vals);
+  write_tile(lk, lv, m, lbase, goff, [&](uint32_t key) { return key >> shift; }, kf, keys, vals);
 }
 
 // compile-time plans of the pass-1 kernels: the fixed-base table windows (n = 2^20..2^26) and
@@ -312,7 +355,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
 struct Pass1Plan {
   int tile, c, W;
   void (*count)(DigitArgs, int, int, size_t, uint32_t *);
-  void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, uint32_t *, uint32_t *);
+  void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, int, uint32_t *, uint32_t *);
   int spt;
 };
 #define TNS_P1(T, C, W, SPT) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT}
@@ -353,6 +396,7 @@ struct PassGeom {
   int ident;              // every segment is one tile: tile g = segment g (tbase / desc unused)
   const uint32_t *mbase;  // set: the counts hold only segments of >= 2 tiles, segment s's block at
                           // nbins * mbase[s] (exclusive scan of their tile counts); else at nbins * tbase[s]
+  int kin, kout;          // key formats read and written (KF_*)
 };
 
 // the first count slot of segment s (its first tile tb)
@@ -399,11 +443,17 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
   constexpr int IPT = TILE / BS_BLOCK;
   const size_t a = G.seg[s] + (size_t)k * TILE, e = min((size_t)G.seg[s + 1], a + TILE);
   uint32_t kk[IPT];
+  // the format branch outside the loads: one branch per load would serialise them
+  auto loads = [&](auto kin) {
 #pragma unroll
-  for (int j = 0; j < IPT; j++) {
-    const size_t p = a + threadIdx.x + (size_t)j * BS_BLOCK;
-    kk[j] = p < e ? keys[p] : 0;
-  }
+    for (int j = 0; j < IPT; j++) {
+      const size_t p = a + threadIdx.x + (size_t)j * BS_BLOCK;
+      kk[j] = p < e ? load_key(decltype(kin)::value, keys, p) : 0;
+    }
+  };
+  if (G.kin == KF_U32) loads(std::integral_constant<int, KF_U32>());
+  else if (G.kin == KF_U16) loads(std::integral_constant<int, KF_U16>());
+  else loads(std::integral_constant<int, KF_U16S>());
 #pragma unroll
   for (int j = 0; j < IPT; j++)
     if (a + threadIdx.x + (size_t)j * BS_BLOCK < e) atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
@@ -465,14 +515,19 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
   const size_t a = s0 + (size_t)k * TILE, e = min((size_t)G.seg[s + 1], a + TILE);
   const int m = (int)(e - a);
   uint32_t kk[IPT], vv[IPT], rk[IPT];
+  auto loads = [&](auto kin) {  // (the format branch outside the loads, as in k_bs_count)
 #pragma unroll
-  for (int j = 0; j < IPT; j++) {
-    const int q = threadIdx.x + j * BS_BLOCK;
-    if (q < m) {
-      kk[j] = keys[a + q];
-      if (PK != 2) vv[j] = vals[a + q];
+    for (int j = 0; j < IPT; j++) {
+      const int q = threadIdx.x + j * BS_BLOCK;
+      if (q < m) {
+        if (PK == 2) kk[j] = keys[a + q];
+        else load_entry(decltype(kin)::value, keys, vals, a + q, kk[j], vv[j]);
+      }
     }
-  }
+  };
+  if (PK == 2 || G.kin == KF_U32) loads(std::integral_constant<int, KF_U32>());
+  else if (G.kin == KF_U16) loads(std::integral_constant<int, KF_U16>());
+  else loads(std::integral_constant<int, KF_U16S>());
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < IPT; j++)
@@ -498,8 +553,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     const uint32_t d = (key >> G.shift) & G.mask;
     const uint32_t pos = goff[d] + (uint32_t)slot - lbase[d];
     if (PK == 0) {
-      okeys[pos] = key;
-      ovals[pos] = lv[slot];
+      store_entry(G.kout, okeys, ovals, pos, key, lv[slot]);
     } else if (PK == 3) {
       ovals[pos] = lv[slot];
     } else if (PK == 1) {
@@ -634,6 +688,23 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   J.ibits = ibits;
   J.shared = shared;
   J.stride = stride;
+  // key formats between passes: 2-byte keys into the last pass (its <= 9 key bits; C4 openings:
+  // pass 2 -> 3, sort kernels -0.6 ms per step, profiles/r03_ab_sort_k16.txt).  TNS_BS_K16=2
+  // also shrinks the earlier passes' keys (17 bits left after pass 1: one of them in the value's
+  // bit 30, free when the values stay below 2^30) -- measured SLOWER (pass 1 +0.2 ms, pass 2
+  // +0.35 ms per opening: half-dword stores of ~64-byte runs), so A/B only; =0: 4-byte keys.
+  const char *k16e = getenv("TNS_BS_K16");
+  const bool k16 = J.vo && !(k16e && k16e[0] == '0');  // (keys + values out: full keys)
+  const bool bit30 = (shared ? (uint64_t)(W - 1) * stride + n : (uint64_t)n) <= ((uint64_t)1 << 30);
+  const bool kall = k16e && k16e[0] == '2';  // every pass (A/B)
+  for (int p = 0, rest = keybits; p < npass - 1; p++) {
+    rest -= bits[p];
+    J.kf[p] = !k16 || (!kall && p != npass - 2) ? KF_U32
+              : rest <= 16                      ? KF_U16
+              : rest == 17 && bit30 && rest - bits[p + 1] >= 1 ? KF_U16S
+                                                               : KF_U32;
+  }
+  if (J.pk) J.kf[npass - 2] = KF_U32;  // the packed words (pack_entry) are 4-byte
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
@@ -658,9 +729,11 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
   TNS_LAUNCH_CHECK();
   exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
-  if (ct) ct->scatter<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
-  else if (tile1 == 4096) k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
-  else k_bs_scatter1<BS_TILE><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, K[0], V[0]);
+  const int kf1 = npass > 1 ? J.kf[0] : KF_U32;
+  if (ct) ct->scatter<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
+  else if (tile1 == 4096)
+    k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
+  else k_bs_scatter1<BS_TILE><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
   TNS_LAUNCH_CHECK();
   k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
   TNS_LAUNCH_CHECK();
@@ -739,7 +812,9 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
   // packed tail: pass npass - 2 writes packed words, the last pass bins them by their top bits
   const int pk = J.pk ? (J.p == J.npass - 2 ? 1 : J.p == J.npass - 1 ? 2 : 0) : J.vo && J.p == J.npass - 1 ? 3 : 0;
   const PackArgs PA{J.ibits, J.bits[J.npass - 1], J.wb, J.shared ? 1 : 0, J.stride};
-  PassGeom G{J.seg[cur], J.tbase, J.desc, pk == 2 ? J.ibits + 1 : J.shift, nb, (uint32_t)nb - 1, ident, mb};
+  const int kin = J.kf[J.p - 1], kout = J.p < J.npass - 1 ? J.kf[J.p] : KF_U32;
+  PassGeom G{J.seg[cur], J.tbase, J.desc, pk == 2 ? J.ibits + 1 : J.shift, nb, (uint32_t)nb - 1, ident, mb, kin,
+             pk == 0 ? kout : KF_U32};
   uint32_t *counts = J.counts, *offs = J.offs;
   if (!ident) {
     if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot

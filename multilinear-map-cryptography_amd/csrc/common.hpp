@@ -489,6 +489,7 @@ struct BucketSortJob {
   bool pk = false, vo = false, shared = false;  // vo: the last pass writes values only
   int ibits = 0, p = 0;
   uint32_t stride = 0;
+  int kf[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key format pass p writes (bucket_sort.hip KF_*)
 };
 void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                        int bucket_bits, uint32_t *valid, BucketSortJob &J);

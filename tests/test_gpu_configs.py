@@ -157,7 +157,7 @@ def test_twist_msm_sort_variant_same_proof():
     assert s_cub == ts.Shout(pp).prove_arrays(entries, idx)
 
 
-@pytest.mark.parametrize("var", ["TNS_BS_PACK", "TNS_BS_VO"])
+@pytest.mark.parametrize("var", ["TNS_BS_PACK", "TNS_BS_VO", "TNS_BS_K16"])
 @pytest.mark.parametrize("L", [14, 18])
 def test_twist_packed_sort_tail_same_proof(L, var, monkeypatch):
     """The packed sort tail (the last pass reads one word per entry and writes values only; the

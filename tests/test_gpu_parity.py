@@ -163,7 +163,8 @@ def test_msm_window_tables_equal_per_window_layout(logn):
 
 
 @pytest.mark.parametrize("variant", ["TNS_BS_RUNTIME_PASS1", "TNS_BS_NO_LOCAL_LAST", "TNS_MSM_W1", "TNS_FIX_WAVES",
-                                     "TNS_BS_TILES", "TNS_MASKED_TREE", "TNS_ACC_ROUNDS", "TNS_BS_PACK", "TNS_BS_VO"])
+                                     "TNS_BS_TILES", "TNS_MASKED_TREE", "TNS_ACC_ROUNDS", "TNS_BS_PACK", "TNS_BS_VO", "TNS_BS_K16",
+                                     "TNS_BS_K16=2"])
 @pytest.mark.parametrize("pattern", ["full", "addr21", "addr22", "val30", "equal"])
 def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     """The bucket sort's fast paths == its general kernels: the compile-time-plan pass 1 (c = 20,
@@ -178,7 +179,9 @@ def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     rule (32), and the packed sort tail (one word per entry into the last pass, values only out
     of it, runs found from the bucket starts) vs keys and values throughout (TNS_BS_PACK=0; the
     table stride here is 2^20 + 1, so the packed index is recovered by a multiply), and the
-    values-only last pass vs keys + values out of it (TNS_BS_VO=0: the accumulation reads keys)."""
+    values-only last pass vs keys + values out of it (TNS_BS_VO=0: the accumulation reads keys),
+    and 16-bit keys into the last pass vs 32-bit ones (TNS_BS_K16=0) or 16-bit keys out of every
+    pass, the 17th key bit of pass 1's output carried in bit 30 of the value (TNS_BS_K16=2)."""
     pp, _ = params(18)
     n = 1 << 20
     rng = np.random.default_rng(len(pattern))
@@ -190,9 +193,10 @@ def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
         bits = int(pattern[-2:])
         c = ts.fr_from_u64_array(rng.integers(0, 1 << bits, size=n, dtype=np.uint64))
     a = ts.msm(pp.commitment_params, c)
-    value = {"TNS_MSM_W1": "0", "TNS_FIX_WAVES": "0", "TNS_BS_PACK": "0", "TNS_BS_VO": "0", "TNS_MASKED_TREE": "0", "TNS_BS_TILES": "4096,8192,4096",
+    value = {"TNS_MSM_W1": "0", "TNS_FIX_WAVES": "0", "TNS_BS_PACK": "0", "TNS_BS_VO": "0", "TNS_BS_K16": "0", "TNS_MASKED_TREE": "0", "TNS_BS_TILES": "4096,8192,4096",
              "TNS_ACC_ROUNDS": "0" if pattern == "full" else "1"}
-    monkeypatch.setenv(variant, value.get(variant, "1"))
+    name, _, forced = variant.partition("=")
+    monkeypatch.setenv(name, forced or value.get(variant, "1"))
     b = ts.msm(pp.commitment_params, c)
     assert a == b
 
