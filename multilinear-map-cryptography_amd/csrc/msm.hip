@@ -1095,9 +1095,16 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sb, hipEventDisableTiming));
+  hipEvent_t acc_a_early = nullptr;  // lane 0's accumulation, queued before lane 1's sort
   if (sorted) {  // staggered: lane 1 sorts under lane 0's accumulation
     msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sorted);
     TNS_HIP(hipEventRecord(sa, l0.stream));
+    // the accumulation goes in before lane 1's sort reaches its host wait (the last pass's
+    // readback): queued after it, lane 1's first passes would run alone
+    if (ja.sorted) {
+      TNS_HIP(hipEventCreateWithFlags(&acc_a_early, hipEventDisableTiming));
+      msm_launch_accumulate(ctx, ja, acc_a_early);
+    }
     TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
     (void)hipEventDestroy(sorted);
     msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
@@ -1139,10 +1146,12 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     // slots from the second accumulation; after it the two tails (short chains, few waves each)
     // run side by side.  (The commitments keep lane 0's tail under lane 1's accumulation: the
     // 22-bit address MSM's 2^22-bucket reduction is longer than the value accumulation.)
-    hipEvent_t acc_a, acc_b;
-    TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+    hipEvent_t acc_a = acc_a_early, acc_b;
+    if (!acc_a) {
+      TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+      msm_launch_accumulate(ctx, ja, acc_a);
+    }
     TNS_HIP(hipEventCreateWithFlags(&acc_b, hipEventDisableTiming));
-    msm_launch_accumulate(ctx, ja, acc_a);
     TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
     msm_launch_accumulate(ctx, jb, acc_b);
     TNS_HIP(hipStreamWaitEvent(l0.stream, acc_b, 0));
@@ -1150,6 +1159,11 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     (void)hipEventDestroy(acc_b);
     msm_launch_tail(ctx, ja);
     msm_launch_tail(ctx, jb);
+  } else if (acc_a_early) {  // lane 0's accumulation is queued: its tail, then lane 1's MSM
+    msm_launch_tail(ctx, ja);
+    if (ctx->msm_serial) TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a_early, 0));
+    (void)hipEventDestroy(acc_a_early);
+    msm_launch_reduce(ctx, jb);
   } else if (ctx->msm_serial) {
     hipEvent_t acc_a;
     TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
