@@ -46,6 +46,17 @@ def test_siphash24_reference_vectors():
         assert L.orc_siphash(buf, n, 0, 0, 1, 3) == po.siphash(m, 0, 0, 1, 3)
 
 
+def test_siphash13_known_answer():
+    # SipHash-1-3 (Rust std DefaultHasher's compression/finalisation rounds), key 00..0f, empty
+    # message: the first vector of Rust's own SipHasher13 suite (library/core/tests/hash/sip.rs,
+    # test_siphash_1_3), bytes dc c4 0f 05 58 01 ac ab.  Both restatements must hit it.
+    k0, k1 = struct.unpack("<QQ", bytes(range(16)))
+    want = int.from_bytes(bytes.fromhex("dcc40f055801acab"), "little")
+    assert po.siphash(b"", k0, k1, 1, 3) == want
+    buf = (co.C.c_uint8 * 1)(0)
+    assert co.lib().orc_siphash(buf, 0, k0, k1, 1, 3) == want
+
+
 def test_fr_rand_rejection_and_montgomery_semantics():
     rng = po.ChaCha20Rng(bytes([42] * 32))
     t = po.fr_rand(rng)
