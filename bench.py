@@ -66,10 +66,14 @@ def parse():
     mode.add_argument("--strong", action="store_true", help="C5 (one 2^26-op proof) at every N, N = 1 included")
     mode.add_argument("--weak", action="store_true", help="2^24 operations per GPU: one N * 2^24-op proof")
     ap.add_argument("--no-extras", action="store_true", help="skip C2/C3 extras and the CPU baseline")
-    ap.add_argument("--cpu-baseline-ops", type=int, default=256,
-                    help="reference-algorithm oracle sample size (C1: 256)")
-    ap.add_argument("--cpu-fast-log-ops", type=int, default=22,
-                    help="fast CPU baseline sample: one proof of 2^k operations (setup_params(k - 2))")
+    ap.add_argument("--cpu-ref-logs", default="4-9",
+                    help="reference-algorithm oracle: time one proof at each 2^k ops, k in this range (a-b); "
+                         "the O(N^3) time is fitted by a power law and extrapolated to 2^24 (labelled)")
+    ap.add_argument("--cpu-fast-log-ops", type=int, default=24,
+                    help="fast CPU baseline: one proof of 2^k operations (setup_params(k - 2)); 24 = C4 itself")
+    ap.add_argument("--sumcheck-logs", default="20,24",
+                    help="generic sum-check extra: degree-3 composition of three 2^k tables, for each k "
+                         "(empty: skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="fast CPU baseline threads (0: every core the process's affinity allows)")
     ap.add_argument("--dropin-steps", type=int, default=None,
@@ -206,23 +210,40 @@ def roofline_from_profile(ts, ctx):
     return roof, stages
 
 
-def cpu_reference_algorithms(n_ops):
-    """The C oracle (reference algorithms: O(N^3) Lagrange, per-term commit, closure sum-check)."""
+def cpu_reference_algorithms(logs):
+    """The C oracle restating the reference algorithms (O(N^3) Lagrange interpolation, per-term
+    commit, closure sum-check; single-threaded as the reference's .iter()) timed on one proof of
+    the ProtocolBenchmarks trace at each 2^k ops (setup_params(k), MemoryTrace::new(2^k)), a power
+    law t = a N^b fitted to the three largest sizes and extrapolated -- labelled as such -- to
+    C4's 2^24 operations (baseline (1))."""
     from oracle import coracle as co
     from oracle import pyoracle as po
 
-    # C1 shape: setup_params(8), MemoryTrace::new(256), 256 ops (memory size = op count)
-    L = max(0, (n_ops - 1).bit_length())
-    cp = co.setup_params(L)
-    ops = po.benchmark_trace(1 << L, n_ops)
-    t0 = time.perf_counter()
-    st, _ = co.twist_prove(cp, ops)
-    dt = time.perf_counter() - t0
-    assert st == 0
-    return {"value": round(n_ops / dt, 3), "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": f"Twist::prove of the {n_ops}-op ProtocolBenchmarks trace (setup_params({L})) by the "
+    pts = []
+    for k in logs:
+        n_ops = 1 << k
+        cp = co.setup_params(k)
+        ops = po.benchmark_trace(n_ops, n_ops)
+        t0 = time.perf_counter()
+        st, _ = co.twist_prove(cp, ops)
+        dt = time.perf_counter() - t0
+        assert st == 0
+        pts.append((k, dt))
+    fit = pts[-3:] if len(pts) >= 3 else pts
+    xs = np.array([k * np.log(2.0) for k, _ in fit])
+    ys = np.log(np.array([t for _, t in fit]))
+    b, a = np.polyfit(xs, ys, 1) if len(fit) > 1 else (3.0, ys[0] - 3.0 * xs[0])
+    t24 = float(np.exp(a + b * 24 * np.log(2.0)))
+    k_last, t_last = pts[-1]
+    return {"value": round((1 << k_last) / t_last, 3), "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": f"Twist::prove of the 2^{k_last}-op ProtocolBenchmarks trace (setup_params({k_last})) by the "
                       f"single-threaded C oracle restating the reference algorithms (O(N^3) interpolation); "
-                      f"{dt:.2f} s"}
+                      f"{t_last:.2f} s",
+            "measured": [{"log_ops": k, "s": round(t, 4), "ops_per_sec": round((1 << k) / t, 3)} for k, t in pts],
+            "fit": {"exponent": round(float(b), 3), "points": [k for k, _ in fit], "law": "t = a * N^b"},
+            "extrapolated_2^24": {"s": round(t24, 1), "days": round(t24 / 86400, 1),
+                                  "ops_per_sec": float(f"{(1 << 24) / t24:.4g}"),
+                                  "note": "EXTRAPOLATED from the fit, not measured"}}
 
 
 def host_cores():
@@ -244,7 +265,7 @@ def host_cores():
     return n, f"affinity {aff} CPUs, cgroup quota {quota if quota else 'none'} CPUs"
 
 
-def cpu_baseline(ts, ctx, log_ops, threads=0, gpu_check=True):
+def cpu_baseline(ts, ctx, log_ops, threads=0, gpu_check=True, pp=None):
     """Fast CPU baseline (SURVEY 8(d) 'fast-CPU'): oracle/fastcpu.c proves Twist with the GPU
     path's algorithms (Lagrange-basis KZG, Pippenger MSM, fold sum-check) on every host core the
     process may use.  Bounded sample: one 2^log_ops-op proof of the src/benchmarks.rs:88-99 trace
@@ -254,7 +275,8 @@ def cpu_baseline(ts, ctx, log_ops, threads=0, gpu_check=True):
 
     n = 1 << log_ops
     L = log_ops - 2
-    pp, _ = ts.setup_params(L, device=ctx.device)
+    if pp is None or pp.log_size != L:
+        pp, _ = ts.setup_params(L, device=ctx.device)
     pp.commitment_params.srs.prepare_lagrange(n)
     addr, val, isw = ts.bench_trace(1 << L, n)
     lag = pp.commitment_params.srs.lagrange_points(n)
@@ -281,6 +303,71 @@ def cpu_baseline(ts, ctx, log_ops, threads=0, gpu_check=True):
     return out
 
 
+def sumcheck_generic(ts, ctx, logs):
+    """SumCheck::prove (src/sumcheck.rs:56-110) of a non-zero degree-3 composition -- the Twist MLE
+    shapes A V - O O V + 2 O over three random 2^k-entry tables resident in HBM -- timed end to
+    end (k rounds: fused fold + round sums on the device, transcript on the host), with the round
+    kernels' HIP-event time and algorithmic bytes (48 B per input entry and table once folded,
+    32 B in round 0) giving their achieved GB/s against the 8 TB/s HBM peak."""
+    R = ts.R_MOD
+    terms = [(1, [0, 1]), (R - 1, [2, 2, 1]), (2, [2])]
+    out = {}
+    rng = np.random.default_rng(9)
+    for k in logs:
+        n = 1 << k
+        tabs = []
+        for _ in range(3):
+            t = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * np.uint64(2)
+            t[:, 3] &= np.uint64((1 << 60) - 1)
+            tabs.append(ts.DeviceBuffer(ctx, t))
+            del t
+        claim = ts.SumCheck.composition_sum_resident(k, tabs, terms)
+        sc = ts.SumCheck(k, claim)
+        sc.prove_resident(tabs, terms, ts.Transcript(bytes(32)), raw=True)  # warm-up
+        reps = 3
+        ts.profile_enable(ctx, True)
+        ts.profile_only(ctx, "sumcheck_round")
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            sc.prove_resident(tabs, terms, ts.Transcript(bytes(32)), raw=True)
+        dt = (time.perf_counter() - t0) / reps
+        ex = ts.profile_read_ex(ctx, "sumcheck_round")
+        ts.profile_only(ctx, None)
+        ts.profile_enable(ctx, False)
+        kms = ex["ms"] / reps
+        gbs = ex["bytes"] / reps / (kms / 1e3) / 1e9 if kms else None
+        out[f"2^{k}"] = {"ms": round(dt * 1e3, 3), "tables": 3, "degree": 3, "rounds": k,
+                         "entries_per_sec": round(3 * n / dt, 1),
+                         "kernel_ms": round(kms, 3), "kernel_launches": ex["launches"] // reps,
+                         "alg_bytes": ex["bytes"] / reps,
+                         "achieved_GBps": round(gbs, 1) if gbs else None,
+                         "hbm_frac": round(gbs / HBM_PEAK_GBPS, 4) if gbs else None,
+                         "bound": "Fr multiply (6 products per composition point x 4 points + 2 per fold)"}
+        del tabs
+    return out
+
+
+def sharded_msm(ts, ctx, comm, pg, local, rank, world, reps=10):
+    """C2 at N ranks: KZGCommitment::commit of 2^20 Fr::rand scalars (ChaCha20Rng([7;32]),
+    setup_params(18)) sharded over the ranks (tns_msm_sharded: per-rank partial MSM over its SRS
+    share, allgather of the 96-byte partials); pairs/s = 2^20 / max over ranks of the time."""
+    n = 1 << 20
+    pp18, _ = ts.setup_params_shard(18, rank, world, ctx=ctx)
+    first, cnt = ts.shard_slice(n, rank, world)
+    sc = ts.fr_rand_batch(bytes([7] * 32), n)[first:first + cnt]
+    d = ts.DeviceBuffer(ctx, np.ascontiguousarray(sc))
+    for _ in range(2):
+        ts.msm_sharded_resident(pp18.commitment_params, comm, d, cnt, n)
+    barrier_sync(pg, local)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ts.msm_sharded_resident(pp18.commitment_params, comm, d, cnt, n)
+    barrier_sync(pg, local)
+    dt = max_over_ranks(pg, local, (time.perf_counter() - t0) / reps)
+    return {"msm_pairs_per_sec_2^20": round(n / dt, 1), "msm_ms_2^20": round(dt * 1e3, 3),
+            "msm_2^20_layout": f"2^20 pairs over {world} ranks, {cnt} per rank (tns_msm_sharded)"}
+
+
 def timed_proofs(fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -299,6 +386,7 @@ def main():
 
     ctx = ts.Context.get(local)
     sharded = world > 1 and not args.independent
+    comm_cfg = None
     # operations of ONE proof: C4 (2^24) at N = 1, C5 (2^26, setup_params(24)) at N > 1
     if args.log_ops is not None:
         log_total = args.log_ops + (world.bit_length() - 1 if args.weak and sharded else 0)
@@ -338,6 +426,15 @@ def main():
 
             on_gpu = torch.cuda.is_available() and not args.rehearse_one_gpu
             comm = ts.Comm.torch(device=torch.device("cuda", local) if on_gpu else None)
+        # the rank count each transport itself reports must be --gpus (RCCL: ncclCommCount)
+        info = comm.info()
+        comm_cfg = {"kind": args.comm if args.comm == "rccl" else f"torch.distributed ({pg.get_backend()}) "
+                                                                   "via the host-callback communicator",
+                    "world_size_seen": info["seen_size"], "process_group_world_size": pg.get_world_size(),
+                    "rank": info["rank"]}
+        if info["seen_size"] != args.gpus or pg.get_world_size() != args.gpus or info["size"] != args.gpus:
+            sys.exit(f"bench.py: the communicator sees {info['seen_size']} ranks (process group "
+                     f"{pg.get_world_size()}) but --gpus {args.gpus}")
     else:
         count = n_ops
         addr, val, isw = ts.bench_trace(1 << L, n_ops)
@@ -395,6 +492,7 @@ def main():
                    "scaling_note": "N = 1 proves C4 (the metric's single-GPU config); N > 1 prove ONE C5 trace "
                                    "(2^26 ops, total fixed: strong scaling); --strong proves C5 at N = 1 too, "
                                    "--weak keeps 2^24 ops per GPU"},
+        "comm": comm_cfg,
         "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
         "commit_basis": args.commit_basis,
         "setup_ms": {"setup_params": round(t_setup * 1e3, 1), "lagrange_basis": round(t_lag * 1e3, 1)},
@@ -435,14 +533,19 @@ def main():
         t_sh = timed_proofs(lambda: ts.shout_prove_resident(pp18, d_e, T, d_i, T), 5, 1)
         out["shout_lookups_per_sec_2^20"] = round(T / t_sh, 1)
         out["shout_ms_2^20"] = round(t_sh * 1e3, 3)
+    if sharded and not args.no_extras:  # the MSM half of the metric at N GPUs (C2 sharded)
+        out.update(sharded_msm(ts, ctx, comm, pg, local, rank, world))
+    if rank == 0 and world == 1 and not args.no_extras and args.sumcheck_logs:
+        out["sumcheck_generic"] = sumcheck_generic(ts, ctx, [int(x) for x in args.sumcheck_logs.split(",")])
     if roof is not None:
         out["roofline"] = roof
         out["stages_ms_per_step"] = {k: round(v["ms"] / stage_steps, 3) for k, v in stages.items()}
         out["stages_timed_on"] = ("the timed steps" if args.profile_all_timed or args.stage_steps <= 0
                                   else f"{stage_steps} untimed steps after the timed region")
     if rank == 0 and world == 1 and not args.no_extras:
-        out["cpu_baseline"] = cpu_baseline(ts, ctx, args.cpu_fast_log_ops, args.cpu_threads)
-        out["cpu_reference_algorithms"] = cpu_reference_algorithms(args.cpu_baseline_ops)
+        out["cpu_baseline"] = cpu_baseline(ts, ctx, args.cpu_fast_log_ops, args.cpu_threads, pp=pp)
+        lo, hi = (int(x) for x in args.cpu_ref_logs.split("-"))
+        out["cpu_reference_algorithms"] = cpu_reference_algorithms(range(lo, hi + 1))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if pg is not None:

@@ -106,6 +106,14 @@ int tns_setup_params(tns_ctx *ctx, unsigned log_size, tns_params *out, tns_srs *
 int tns_srs_upload(tns_ctx *ctx, const uint64_t *g1_affine, size_t n, tns_srs **out);
 /* Copy points [0, n) of the SRS to host memory (affine uint64_t[8] each). */
 int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_affine_out, size_t n);
+/* Copy the points g1_powers[idx[t]], t < k, to host memory (affine uint64_t[8] each).  Every
+ * index must lie in this SRS's share (all of g1_powers, or a shard's [first, first + held)):
+ * spot checks of a large (or sharded) SRS without downloading it (CommitmentParams.g1_powers
+ * is a public Vec the reference's own test reads, src/utils.rs:56, :283). */
+int tns_srs_download_indices(tns_ctx *ctx, const tns_srs *srs, const uint64_t *idx, size_t k,
+                             uint64_t *g1_affine_out);
+/* The share of g1_powers this SRS holds: [first, first + held) (0 and tns_srs_len unsharded). */
+int tns_srs_share(const tns_srs *srs, uint64_t *first, uint64_t *held);
 size_t tns_srs_len(const tns_srs *srs);
 void tns_srs_destroy(tns_srs *srs);
 /* Attach the setup trapdoor kept in CommitmentParams.tau (src/utils.rs:60-61, :94-100)
@@ -197,6 +205,14 @@ int tns_sumcheck_prove(tns_ctx *ctx, const uint64_t *const *tables, int n_tables
                        const uint64_t claimed_sum[4], const tns_term *terms, int n_terms,
                        tns_transcript *transcript, uint64_t *rounds_out, uint64_t final_out[4],
                        uint64_t *challenges_out);
+/* The composition's sum over {0,1}^nv (the honest claimed_sum) on device tables. */
+int tns_composition_sum_device(tns_ctx *ctx, const uint64_t *const *d_tables, int n_tables, unsigned nv,
+                               const tns_term *terms, int n_terms, uint64_t out[4]);
+/* The same on tables already resident in HBM (device pointers, only read). */
+int tns_sumcheck_prove_device(tns_ctx *ctx, const uint64_t *const *d_tables, int n_tables, unsigned nv,
+                              const uint64_t claimed_sum[4], const tns_term *terms, int n_terms,
+                              tns_transcript *transcript, uint64_t *rounds_out, uint64_t final_out[4],
+                              uint64_t *challenges_out);
 
 /* ---------------------------------------------------------------- protocols */
 /* Twist::prove (src/twist.rs:107-252).  The MemoryTrace's operations as SoA:
@@ -216,6 +232,8 @@ int tns_shout_prove(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
 typedef struct tns_buffer tns_buffer;
 int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer **out);
 void *tns_buffer_device_ptr(const tns_buffer *buf);
+/* Copy the first `bytes` of the buffer back to host memory. */
+int tns_buffer_download(const tns_buffer *buf, void *host, size_t bytes);
 void tns_buffer_free(tns_buffer *buf);
 int tns_twist_prove_device(tns_ctx *ctx, const tns_srs *srs, const tns_params *params,
                            const uint64_t *d_addr, const uint64_t *d_value,
@@ -284,6 +302,9 @@ int tns_comm_create(tns_ctx *ctx, int rank, int size, const uint8_t uid[128], tn
 /* Communicator over any host-side transport. */
 int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user, tns_comm **out);
 void tns_comm_destroy(tns_comm *comm);
+/* rank and size the communicator was created with, the rank count its transport reports
+ * (ncclCommCount for RCCL, else size) and its kind: 0 one rank, 1 host callback, 2 RCCL. */
+int tns_comm_info(const tns_comm *comm, int *rank, int *size, int *seen_size, int *kind);
 /* The communicator's allgather on its own (self-test / launcher use); ctx may be NULL for a
  * callback communicator. */
 int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv);
@@ -295,6 +316,13 @@ int tns_srs_prepare_lagrange_shard(tns_ctx *ctx, tns_srs *srs, size_t n, int ran
  * tau"); tns_srs_len still reports the full length. */
 int tns_setup_params_shard(tns_ctx *ctx, unsigned log_size, int rank, int size, tns_params *out,
                            tns_srs **srs_out);
+/* KZGCommitment::commit (src/commitments.rs:162-180) of n_total coefficients sharded over the
+ * ranks (the C2 MSM at N GPUs): rank r holds coefficients [r N/size, r N/size + n_local) on the
+ * device (N = next_pow2(n_total); n_local = that slice's length) and an SRS share covering them
+ * (tns_setup_params_shard splits 2^k + 1 powers on those boundaries); one partial MSM per rank,
+ * an allgather of the 96-byte partials.  Every rank returns the whole commitment. */
+int tns_msm_sharded(tns_ctx *ctx, const tns_srs *srs, tns_comm *comm, const uint64_t *d_scalars, size_t n_local,
+                    uint64_t n_total, uint64_t out_proj[12]);
 /* Twist::prove of a trace of n_total operations whose operations
  * [rank * N/size, rank * N/size + n_local) (N = next_pow2(n_total)) this rank holds on the
  * device; n_local must be that slice's length (0 for ranks past the end). */

@@ -395,9 +395,18 @@ static void setup_core(tns_ctx *ctx, unsigned log_size, int rank, int size, tns_
   tns_srs *s = new tns_srs();
   s->s.device = ctx->c.device;
   s->s.n = out->num_powers;
-  const size_t base = s->s.n / size, rem = s->s.n % size;
-  s->s.first = (size_t)rank * base + std::min<size_t>(rank, rem);
-  s->s.held = base + ((size_t)rank < rem ? 1 : 0);
+  // shares of the 2^k + 1 powers: [r 2^k/size, (r + 1) 2^k/size), the last rank also holding
+  // g1_powers[2^k] -- so rank r's share covers the coefficient slice of tns_shard_slice
+  // (tns_msm_sharded); any other count splits as evenly as possible
+  const size_t m = s->s.n - 1;
+  if (m % (size_t)size == 0 && m >= (size_t)size) {
+    s->s.first = (size_t)rank * (m / size);
+    s->s.held = m / size + (rank == size - 1 ? 1 : 0);
+  } else {
+    const size_t base = s->s.n / size, rem = s->s.n % size;
+    s->s.first = (size_t)rank * base + std::min<size_t>(rank, rem);
+    s->s.held = base + ((size_t)rank < rem ? 1 : 0);
+  }
   s->s.has_tau = true;
   s->s.tau = tau;
   try {
@@ -451,6 +460,29 @@ int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_out, size_t 
     if (n) TNS_HIP(hipMemcpy(g1_out, srs->s.points.p, sizeof(G1Affine) * n, hipMemcpyDeviceToHost));
     return TNS_OK;
   });
+}
+
+int tns_srs_download_indices(tns_ctx *ctx, const tns_srs *srs, const uint64_t *idx, size_t k,
+                             uint64_t *g1_out) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    for (size_t t = 0; t < k; t++)
+      if (idx[t] < srs->s.first || idx[t] >= srs->s.first + srs->s.held)
+        throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS index outside this SRS's share");
+    const G1Affine *pts = srs->s.points.as<G1Affine>();
+    for (size_t t = 0; t < k; t++)
+      TNS_HIP(hipMemcpyAsync(g1_out + 8 * t, pts + (idx[t] - srs->s.first), sizeof(G1Affine), hipMemcpyDeviceToHost,
+                             ctx->c.stream));
+    TNS_HIP(hipStreamSynchronize(ctx->c.stream));
+    return TNS_OK;
+  });
+}
+
+int tns_srs_share(const tns_srs *srs, uint64_t *first, uint64_t *held) {
+  if (!srs) return TNS_ERR_INVALID_PARAMETERS;
+  *first = srs->s.first;
+  *held = srs->s.held;
+  return TNS_OK;
 }
 
 size_t tns_srs_len(const tns_srs *srs) { return srs ? srs->s.n : 0; }
@@ -732,13 +764,37 @@ void tns_transcript_challenge_field_element(tns_transcript *t, const uint8_t *la
   std::memcpy(out, &r, 32);
 }
 
+static int sumcheck_prove_core(tns_ctx *ctx, Fr *const *ptrs, int n_tables, unsigned nv, const uint64_t claimed[4],
+                               const tns_term *terms, int n_terms, tns_transcript *tr, uint64_t *rounds_out,
+                               uint64_t final_out[4], uint64_t *challenges_out) {
+  std::vector<SumcheckTerm> st(n_terms);
+  for (int t = 0; t < n_terms; t++) {
+    std::memcpy(&st[t].coeff, terms[t].coeff, 32);
+    for (int j = 0; j < 3; j++) st[t].tab[j] = terms[t].tables[j];
+  }
+  Fr cl;
+  std::memcpy(&cl, claimed, 32);
+  std::vector<Fr> rounds(4 * (size_t)(nv ? nv : 1)), chal(nv ? nv : 1);
+  Fr finals[4], fe;
+  int rc = sumcheck_prove_dev(&ctx->c, ptrs, n_tables, nv, cl, st.data(), n_terms, tr->t, rounds.data(),
+                              chal.data(), finals, &fe);
+  std::memcpy(rounds_out, rounds.data(), 128 * (size_t)nv);
+  if (challenges_out) std::memcpy(challenges_out, chal.data(), 32 * (size_t)nv);
+  std::memcpy(final_out, &fe, 32);
+  return rc;
+}
+
+static void check_sumcheck_shape(unsigned nv, int n_tables, int n_terms) {
+  if (nv > 30 || n_tables < 0 || n_tables > 4 || n_terms < 0)
+    throw Error(TNS_ERR_INVALID_PARAMETERS, "unsupported sum-check shape (<= 4 tables)");
+}
+
 int tns_sumcheck_prove(tns_ctx *ctx, const uint64_t *const *tables, int n_tables, unsigned nv,
                        const uint64_t claimed[4], const tns_term *terms, int n_terms, tns_transcript *tr,
                        uint64_t *rounds_out, uint64_t final_out[4], uint64_t *challenges_out) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
-    if (nv > 30 || n_tables < 0 || n_tables > 4)
-      throw Error(TNS_ERR_INVALID_PARAMETERS, "unsupported sum-check shape (<= 4 tables)");
+    check_sumcheck_shape(nv, n_tables, n_terms);
     size_t n = (size_t)1 << nv;
     std::vector<DevBuf> bufs(n_tables);
     std::vector<Fr *> ptrs(n_tables);
@@ -746,21 +802,39 @@ int tns_sumcheck_prove(tns_ctx *ctx, const uint64_t *const *tables, int n_tables
       ptrs[i] = (Fr *)bufs[i].ensure(sizeof(Fr) * n);
       TNS_HIP(hipMemcpyAsync(ptrs[i], tables[i], sizeof(Fr) * n, hipMemcpyHostToDevice, ctx->c.stream));
     }
+    return sumcheck_prove_core(ctx, ptrs.data(), n_tables, nv, claimed, terms, n_terms, tr, rounds_out, final_out,
+                               challenges_out);
+  });
+}
+
+int tns_composition_sum_device(tns_ctx *ctx, const uint64_t *const *d_tables, int n_tables, unsigned nv,
+                               const tns_term *terms, int n_terms, uint64_t out[4]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    check_sumcheck_shape(nv, n_tables, n_terms);
+    std::vector<Fr *> ptrs(n_tables);
+    for (int i = 0; i < n_tables; i++) ptrs[i] = (Fr *)d_tables[i];
     std::vector<SumcheckTerm> st(n_terms);
     for (int t = 0; t < n_terms; t++) {
       std::memcpy(&st[t].coeff, terms[t].coeff, 32);
       for (int j = 0; j < 3; j++) st[t].tab[j] = terms[t].tables[j];
     }
-    Fr cl;
-    std::memcpy(&cl, claimed, 32);
-    std::vector<Fr> rounds(4 * (size_t)(nv ? nv : 1)), chal(nv ? nv : 1);
-    Fr finals[4], fe;
-    int rc = sumcheck_prove_dev(&ctx->c, ptrs.data(), n_tables, nv, cl, st.data(), n_terms, tr->t,
-                                rounds.data(), chal.data(), finals, &fe);
-    std::memcpy(rounds_out, rounds.data(), 128 * (size_t)nv);
-    if (challenges_out) std::memcpy(challenges_out, chal.data(), 32 * (size_t)nv);
-    std::memcpy(final_out, &fe, 32);
-    return rc;
+    const Fr s = composition_sum_dev(&ctx->c, ptrs.data(), n_tables, nv, st.data(), n_terms);
+    std::memcpy(out, &s, 32);
+    return TNS_OK;
+  });
+}
+
+int tns_sumcheck_prove_device(tns_ctx *ctx, const uint64_t *const *d_tables, int n_tables, unsigned nv,
+                              const uint64_t claimed[4], const tns_term *terms, int n_terms, tns_transcript *tr,
+                              uint64_t *rounds_out, uint64_t final_out[4], uint64_t *challenges_out) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    check_sumcheck_shape(nv, n_tables, n_terms);
+    std::vector<Fr *> ptrs(n_tables);
+    for (int i = 0; i < n_tables; i++) ptrs[i] = (Fr *)d_tables[i];  // only read
+    return sumcheck_prove_core(ctx, ptrs.data(), n_tables, nv, claimed, terms, n_terms, tr, rounds_out, final_out,
+                               challenges_out);
   });
 }
 
@@ -1461,6 +1535,17 @@ int tns_comm_create_callback(int rank, int size, tns_allgather_fn fn, void *user
 
 void tns_comm_destroy(tns_comm *comm) { delete comm; }
 
+int tns_comm_info(const tns_comm *comm, int *rank, int *size, int *seen_size, int *kind) {
+  return guarded([&]() {
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    if (rank) *rank = comm->c->rank;
+    if (size) *size = comm->c->size;
+    if (seen_size) *seen_size = comm->c->seen_size();
+    if (kind) *kind = comm->c->kind();
+    return TNS_OK;
+  });
+}
+
 int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv) {
   return guarded([&]() {
     if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
@@ -1504,6 +1589,14 @@ int tns_buffer_upload(tns_ctx *ctx, const void *host, size_t bytes, tns_buffer *
   });
 }
 void *tns_buffer_device_ptr(const tns_buffer *b) { return b ? b->buf.p : nullptr; }
+int tns_buffer_download(const tns_buffer *b, void *host, size_t bytes) {
+  return guarded([&]() {
+    if (!b || bytes > b->bytes) throw Error(TNS_ERR_INVALID_PARAMETERS, "download beyond the buffer");
+    TNS_HIP(hipSetDevice(b->device));
+    if (bytes) TNS_HIP(hipMemcpy(host, b->buf.p, bytes, hipMemcpyDeviceToHost));
+    return TNS_OK;
+  });
+}
 void tns_buffer_free(tns_buffer *b) {
   if (!b) return;
   (void)hipSetDevice(b->device);
@@ -1514,6 +1607,30 @@ int tns_msm_device(tns_ctx *ctx, const tns_srs *srs, const uint64_t *d_scalars, 
   return guarded([&]() {
     CtxScope g(&ctx->c);
     store_proj(commit_dev(&ctx->c, srs->s, (const Fr *)d_scalars, n), out);
+    return TNS_OK;
+  });
+}
+
+int tns_msm_sharded(tns_ctx *ctx, const tns_srs *srs, tns_comm *comm, const uint64_t *d_scalars, size_t n_local,
+                    uint64_t n_total, uint64_t out[12]) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    Comm &m = *comm->c;
+    if (n_total > srs->s.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
+    const size_t N = next_pow2((size_t)n_total);
+    check_shard(m, N, "coefficient");
+    const size_t L = N / (size_t)m.size, first = (size_t)m.rank * L;
+    if (n_local != slice_count(n_total, first, L))
+      throw Error(TNS_ERR_INVALID_PARAMETERS, "n_local is not this rank's slice of n_total");
+    if (n_local && (first < srs->s.first || first + n_local > srs->s.first + srs->s.held))
+      throw Error(TNS_ERR_INVALID_PARAMETERS, "this rank's SRS share does not hold its coefficient slice");
+    const size_t off = first - std::min(first, srs->s.first);
+    const FixedBase *fb = srs_fixed_base(&ctx->c, srs->s, n_local);
+    const G1Xyzz part = n_local ? msm_dev(&ctx->c, srs->s.points.as<G1Affine>() + off, (const Fr *)d_scalars, n_local,
+                                          fb, off)
+                                : G1Xyzz::inf();
+    store_proj(xyzz_to_affine(allgather_sum_g1(&ctx->c, m, part)), out);
     return TNS_OK;
   });
 }

@@ -24,12 +24,14 @@ namespace tns {
 namespace {
 
 struct SelfComm final : Comm {
+  int kind() const override { return 0; }
   void allgather(Ctx *, const void *send, size_t bytes, void *recv) override { std::memcpy(recv, send, bytes); }
 };
 
 struct CallbackComm final : Comm {
   tns_allgather_fn fn;
   void *user;
+  int kind() const override { return 1; }
   void allgather(Ctx *, const void *send, size_t bytes, void *recv) override {
     const int st = fn(user, send, bytes, recv);
     if (st != 0) throw Error(TNS_ERR_DEVICE, "allgather callback failed with status " + std::to_string(st));
@@ -47,6 +49,12 @@ struct RcclComm final : Comm {
   DevBuf send_b, recv_b;
   ~RcclComm() override {
     if (comm) (void)ncclCommDestroy(comm);
+  }
+  int kind() const override { return 2; }
+  int seen_size() const override {
+    int n = 0;
+    TNS_NCCL(ncclCommCount(comm, &n));
+    return n;
   }
   void allgather(Ctx *c, const void *send, size_t bytes, void *recv) override {
     if (!c) throw Error(TNS_ERR_INVALID_PARAMETERS, "the RCCL communicator needs a context");

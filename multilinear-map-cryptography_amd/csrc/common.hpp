@@ -366,6 +366,7 @@ struct HostTranscript;
 bool sumcheck_folds_take_flag_bytes(unsigned nv);
 void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
                                Fr *d_out, const uint8_t *flags = nullptr, size_t n_flags = 0);
+Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const SumcheckTerm *terms, int n_terms);
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_table_values, Fr *final_eval);
@@ -381,7 +382,9 @@ void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
-G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr);
+// fb_off: the points are entries [fb_off, fb_off + n) of the set fb was built for
+G1Xyzz msm_dev(Ctx *c, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb = nullptr,
+               size_t fb_off = 0);
 // bit length of a canonical field element (0 for zero)
 __device__ __forceinline__ unsigned fr_bit_length(const Fr &k) {
   unsigned b = 0;
@@ -534,6 +537,10 @@ bool fr_is_node(const Fr &x, size_t N);
 struct Comm {
   int rank = 0, size = 1;
   virtual ~Comm() = default;
+  // 0 = one rank (self), 1 = host callback, 2 = RCCL
+  virtual int kind() const = 0;
+  // the rank count the transport itself reports (ncclCommCount for RCCL)
+  virtual int seen_size() const { return size; }
   // every rank's `bytes` from `send`, in rank order, into recv (size * bytes)
   virtual void allgather(Ctx *c, const void *send, size_t bytes, void *recv) = 0;
 };

@@ -363,6 +363,42 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   TNS_LAUNCH_CHECK();
 }
 
+// sum over {0,1}^nv of the composition (the honest prover's claimed sum): round 0's sums at
+// X = 0 and X = 1 of the fused round kernel, added
+Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const SumcheckTerm *terms, int n_terms) {
+  if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "1 to 4 sum-check tables");
+  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
+  ScTerms st{};
+  st.n = n_terms;
+  for (int t = 0; t < n_terms; t++) {
+    st.coeff[t] = terms[t].coeff;
+    for (int j = 0; j < 3; j++) {
+      if (terms[t].tab[j] >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
+      st.tab[t][j] = (int8_t)terms[t].tab[j];
+    }
+  }
+  if (nv == 0) {
+    Fr v[MAX_SC_TABLES];
+    for (int i = 0; i < k; i++) TNS_HIP(hipMemcpyAsync(&v[i], tables[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipStreamSynchronize(c->stream));
+    return eval_composition_host(v, terms, n_terms);
+  }
+  const size_t P = (size_t)1 << (nv - 1);
+  const unsigned g = grid_for(P, 256, 2048);
+  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * (size_t)g, 64));
+  Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
+  ScTables tt{};
+  for (int i = 0; i < k; i++) tt.in[i] = tables[i];
+  k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, Fr::zero(), partials);
+  TNS_LAUNCH_CHECK();
+  k_sum_partials4<<<1, 256, 0, c->stream>>>(partials, (int)g, sums_dev);
+  TNS_LAUNCH_CHECK();
+  Fr e[4];
+  TNS_HIP(hipMemcpyAsync(e, sums_dev, sizeof e, hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  return add(e[0], e[1]);
+}
+
 // SumCheck::prove (src/sumcheck.rs:56-110) for an MLE composition.
 // tables: k device arrays of 2^nv Fr (read only).  Host transcript drives challenges.
 int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,

@@ -641,7 +641,7 @@ FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n) {
 
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n) {
   if (n < ((size_t)1 << 16) || !c->msm_tables) return nullptr;
-  if (srs.first != 0 || srs.held < n) return nullptr;
+  if (srs.held < n) return nullptr;  // a shard's table covers its held points (tns_msm_sharded)
   if (!srs.fb) srs.fb = fixed_base_build_dev(c, srs.points.as<G1Affine>(), srs.held);
   return srs.fb;
 }
@@ -1003,7 +1003,7 @@ static G1Xyzz msm_complete(Ctx *ctx, MsmJob &J) {
   return acc;
 }
 
-G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb) {
+G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, const FixedBase *fb, size_t fb_off) {
   if (n == 0) return G1Xyzz::inf();
   MsmLane &ln = ctx->lanes[0];
   unsigned bits = 254;
@@ -1013,7 +1013,8 @@ G1Xyzz msm_dev(Ctx *ctx, const G1Affine *points, const Fr *scalars, size_t n, co
     bits = bits_result(ln);
   }
   MsmJob J;
-  msm_launch(ctx, ln, points, scalars, in, n, fb, bits, J);
+  msm_launch_sort(ctx, ln, points, scalars, in, n, fb, bits, J, nullptr, false, fb_off);
+  msm_launch_reduce(ctx, J);
   return msm_complete(ctx, J);
 }
 

@@ -225,7 +225,24 @@ class Srs:
         _check(N.load().tns_srs_download(self.ctx.handle, self.handle, N.p64(out), n))
         return out
 
+    def share(self) -> Tuple[int, int]:
+        """(first, held): the slice of g1_powers this SRS holds (a shard's share, or all of it)."""
+        a, b = C.c_uint64(), C.c_uint64()
+        _check(N.load().tns_srs_share(self.handle, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def points_at(self, indices) -> np.ndarray:
+        """g1_powers[i] for the given global indices (affine Montgomery limbs), within share()."""
+        idx = np.ascontiguousarray(indices, dtype=np.uint64)
+        out = np.zeros((len(idx), 8), dtype=np.uint64)
+        if len(idx):
+            _check(N.load().tns_srs_download_indices(self.ctx.handle, self.handle, N.p64(idx), len(idx),
+                                                     N.p64(out)))
+        return out
+
     def __del__(self):
+        if _EXITING:  # the HIP runtime may already be gone (as Context.__del__)
+            return
         try:
             N.load().tns_srs_destroy(self.handle)
         except Exception:
@@ -703,6 +720,47 @@ class SumCheck:
             return proof, from_mont(ch[:nv]) if nv else []
         return proof
 
+    @staticmethod
+    def _terms(terms):
+        tt = (N.TnsTerm * max(1, len(terms)))()
+        for i, (coef, idx) in enumerate(terms):
+            tt[i].coeff = (C.c_uint64 * 4)(*[int(x) for x in to_mont([coef])[0]])
+            tt[i].tables = (C.c_int32 * 3)(*(list(idx) + [-1] * (3 - len(idx))))
+        return tt
+
+    @staticmethod
+    def composition_sum_resident(num_vars: int, tables: Sequence["DeviceBuffer"],
+                                 terms: Sequence[Tuple[int, Sequence[int]]]) -> int:
+        """sum over {0,1}^num_vars of the composition on device tables (the honest claimed sum)."""
+        ptrs = (C.c_void_p * len(tables))(*[t.ptr for t in tables])
+        out = np.zeros(4, dtype=np.uint64)
+        _check(N.load().tns_composition_sum_device(tables[0].ctx.handle, ptrs, len(tables), num_vars,
+                                                   SumCheck._terms(terms), len(terms), N.p64(out)))
+        return from_mont(out)[0]
+
+    def prove_resident(self, tables: Sequence["DeviceBuffer"], terms: Sequence[Tuple[int, Sequence[int]]],
+                       transcript: Transcript, raw: bool = False):
+        """The same proof on tables already resident in HBM (DeviceBuffers of 2^num_vars
+        Montgomery Fr, only read).  raw=True returns the Montgomery arrays (rounds, final,
+        challenges) without converting them (timing loops)."""
+        nv = self.num_vars
+        if not tables:
+            raise InvalidParameters("no tables")
+        ctx = tables[0].ctx
+        for t in tables:
+            if t.nbytes != 32 << nv:
+                raise InvalidParameters("every table needs 2^num_vars entries")
+        ptrs = (C.c_void_p * len(tables))(*[t.ptr for t in tables])
+        cl = to_mont([self.claimed_sum])[0]
+        rounds = np.zeros((max(1, nv), 4, 4), dtype=np.uint64)
+        fin = np.zeros(4, dtype=np.uint64)
+        ch = np.zeros((max(1, nv), 4), dtype=np.uint64)
+        _check(N.load().tns_sumcheck_prove_device(ctx.handle, ptrs, len(tables), nv, N.p64(cl), self._terms(terms),
+                                                  len(terms), transcript._h, N.p64(rounds), N.p64(fin), N.p64(ch)))
+        if raw:
+            return rounds[:nv], fin, ch[:nv]
+        return SumCheckProof([from_mont(r) for r in rounds[:nv]], from_mont(fin)[0]), (from_mont(ch[:nv]) if nv else [])
+
 
 # ----------------------------------------------------------------------------- Twist
 @dataclass(frozen=True)
@@ -1065,10 +1123,18 @@ class DeviceBuffer:
         self.ptr = N.load().tns_buffer_device_ptr(self.handle)
 
     def __del__(self):
+        if _EXITING:
+            return
         try:
             N.load().tns_buffer_free(self.handle)
         except Exception:
             pass
+
+
+def buffer_download(buf: DeviceBuffer, out: np.ndarray):
+    """Copy the buffer's first out.nbytes bytes into the (C-contiguous) host array out."""
+    assert out.flags["C_CONTIGUOUS"]
+    _check(N.load().tns_buffer_download(buf.handle, out.ctypes.data_as(C.c_void_p), out.nbytes))
 
 
 def twist_prove_resident(pp: ProverParams, addr: DeviceBuffer, value: DeviceBuffer, is_write: DeviceBuffer,
@@ -1155,6 +1221,14 @@ class Comm:
             return out.cpu().numpy().tobytes()
         return cls.from_allgather(rank, size, fn)
 
+    KINDS = {0: "self", 1: "callback", 2: "rccl"}
+
+    def info(self) -> dict:
+        """rank, size, the rank count the transport reports (ncclCommCount for RCCL) and kind."""
+        r, n, seen, k = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        _check(N.load().tns_comm_info(self.handle, C.byref(r), C.byref(n), C.byref(seen), C.byref(k)))
+        return {"rank": r.value, "size": n.value, "seen_size": seen.value, "kind": self.KINDS.get(k.value, "?")}
+
     def allgather(self, data: bytes, ctx: Optional[Context] = None) -> bytes:
         """The communicator's own allgather (every rank's bytes, in rank order)."""
         src = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
@@ -1190,6 +1264,18 @@ def shard_slice(n_total: int, rank: int, size: int) -> Tuple[int, int]:
     L = (1 << max(0, (n_total - 1).bit_length())) // size
     first = rank * L
     return first, max(0, min(L, n_total - first))
+
+
+def msm_sharded_resident(params: CommitmentParams, comm: Comm, scalars: DeviceBuffer, n_local: int,
+                         n_total: int) -> np.ndarray:
+    """KZGCommitment::commit of n_total coefficients sharded over comm's ranks (tns_msm_sharded):
+    this rank's slice (shard_slice) resident in HBM, its SRS share from setup_params_shard.
+    Returns the commitment's projective limbs (every rank the same)."""
+    srs = params.srs
+    out = np.zeros(12, dtype=np.uint64)
+    _check(N.load().tns_msm_sharded(srs.ctx.handle, srs.handle, comm.handle, scalars.ptr, n_local, n_total,
+                                    N.p64(out)))
+    return out
 
 
 def twist_prove_sharded_resident(pp: ProverParams, comm: Comm, addr: DeviceBuffer, value: DeviceBuffer,

@@ -77,6 +77,8 @@ SIGNATURES = [
     ("tns_setup_params", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),
     ("tns_srs_upload", C.c_int, [C.c_void_p, U64P, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("tns_srs_download", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t]),
+    ("tns_srs_download_indices", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
+    ("tns_srs_share", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     ("tns_srs_len", C.c_size_t, [C.c_void_p]),
     ("tns_srs_destroy", None, [C.c_void_p]),
     ("tns_srs_set_tau", C.c_int, [C.c_void_p, U64P]),
@@ -103,6 +105,11 @@ SIGNATURES = [
     ("tns_sumcheck_prove", C.c_int,
      [C.c_void_p, C.POINTER(U64P), C.c_int, C.c_uint, U64P, C.POINTER(TnsTerm), C.c_int, C.c_void_p, U64P,
       U64P, U64P]),
+    ("tns_composition_sum_device", C.c_int,
+     [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_uint, C.POINTER(TnsTerm), C.c_int, U64P]),
+    ("tns_sumcheck_prove_device", C.c_int,
+     [C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_uint, U64P, C.POINTER(TnsTerm), C.c_int, C.c_void_p, U64P,
+      U64P, U64P]),
     ("tns_twist_prove", C.c_int,
      [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), U64P, U64P, U8P, C.c_size_t, C.POINTER(TnsProof)]),
     ("tns_shout_prove", C.c_int,
@@ -110,6 +117,7 @@ SIGNATURES = [
     ("tns_buffer_upload", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("tns_buffer_device_ptr", C.c_void_p, [C.c_void_p]),
     ("tns_buffer_free", None, [C.c_void_p]),
+    ("tns_buffer_download", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("tns_twist_prove_device", C.c_int,
      [C.c_void_p, C.c_void_p, C.POINTER(TnsParams), C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
       C.POINTER(TnsProof)]),
@@ -144,6 +152,9 @@ SIGNATURES = [
     ("tns_comm_create", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_void_p)]),
     ("tns_comm_create_callback", C.c_int, [C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("tns_comm_destroy", None, [C.c_void_p]),
+    ("tns_comm_info", C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                C.POINTER(C.c_int)]),
+    ("tns_msm_sharded", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64, U64P]),
     ("tns_comm_allgather", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("tns_srs_prepare_lagrange_shard", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]),
     ("tns_setup_params_shard", C.c_int,

@@ -159,6 +159,44 @@ def sumcheck_prove(tables, nv, claimed, terms, prefix: bytes = b""):
     return st, rounds[:nv], fin, chal[:nv]
 
 
+def _terms_arrays(terms):
+    coeffs = fr_array([c for c, _ in terms]) if terms else np.zeros((1, 4), dtype=np.uint64)
+    tt = np.full((max(1, len(terms)), 3), -1, dtype=np.int32)
+    for i, (_, ix) in enumerate(terms):
+        tt[i, : len(ix)] = ix
+    return coeffs, tt
+
+
+def fast_sumcheck_prove(tables, nv, claimed, terms, prefix: bytes = b"", threads=1):
+    """fastcpu.c fc_sumcheck_prove: the same outputs as sumcheck_prove with O(N)-per-round folds
+    on `threads` host threads.  tables: (2^nv, 4) Montgomery arrays; claimed: int or None (the
+    honest sum, fast_composition_sum)."""
+    arrs = [np.ascontiguousarray(t, dtype=np.uint64).reshape(-1, 4) for t in tables]
+    ptrs = (U64P * max(1, len(arrs)))(*[_p(a) for a in arrs])
+    coeffs, tt = _terms_arrays(terms)
+    if claimed is None:
+        claimed = fast_composition_sum(arrs, nv, terms, threads)
+    cl = fr_array([claimed])[0]
+    rounds = np.zeros((max(1, nv), 4, 4), dtype=np.uint64)
+    fin = np.zeros(4, dtype=np.uint64)
+    chal = np.zeros((max(1, nv), 4), dtype=np.uint64)
+    pre = (C.c_uint8 * max(1, len(prefix))).from_buffer_copy(prefix or b"\0")
+    st = lib().fc_sumcheck_prove(ptrs, C.c_int(len(arrs)), C.c_uint(nv), _p(cl), C.c_int(len(terms)), _p(coeffs),
+                                 tt.ctypes.data_as(C.POINTER(C.c_int)), pre, C.c_size_t(len(prefix)),
+                                 C.c_int(threads), _p(rounds), _p(fin), _p(chal))
+    return st, rounds[:nv], fin, chal[:nv]
+
+
+def fast_composition_sum(tables, nv, terms, threads=1) -> int:
+    arrs = [np.ascontiguousarray(t, dtype=np.uint64).reshape(-1, 4) for t in tables]
+    ptrs = (U64P * max(1, len(arrs)))(*[_p(a) for a in arrs])
+    coeffs, tt = _terms_arrays(terms)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().fc_composition_sum(ptrs, C.c_uint(nv), C.c_int(len(terms)), _p(coeffs),
+                             tt.ctypes.data_as(C.POINTER(C.c_int)), C.c_int(threads), _p(out))
+    return fr_ints(out)[0]
+
+
 def _proof_dict(pr: OrcProof, names):
     nr = pr.num_rounds
     rounds = np.ctypeslib.as_array(pr.round_polynomials)[:nr]

@@ -459,3 +459,187 @@ int fc_twist_prove(const uint64_t *lagrange, const uint64_t *bary_w, size_t N, s
   free(YV);
   return st;
 }
+
+/* ------------------------------------------------------------- SumCheck::prove, O(N) per round */
+/* src/sumcheck.rs:56-110, :156-212 with the closure an MLE composition sum_t c_t prod_j T_{tt[t][j]}
+ * (<= 3 factors, <= FC_SC_TABLES tables): instead of evaluating every MLE at every hypercube
+ * point (oracle.c sumcheck_core, O(N n) per point), each table is folded once per round
+ * (T'[s] = T[2s] + r (T[2s+1] - T[2s]), src/polynomials.rs:111-119) and round k sums the
+ * composition of the values T_k[2s] + X (T_k[2s+1] - T_k[2s]) at X = 0..3.  Same round
+ * polynomials, challenges and final evaluation as orc_sumcheck_prove (tests/test_fastcpu.py). */
+#define FC_SC_TABLES 4
+typedef struct {
+  const u64 *src[FC_SC_TABLES];
+  u64 *dst[FC_SC_TABLES];
+  int k, fold;
+  const u64 *r;
+  int n_terms;
+  const u64 *coeffs;
+  const int *tt;
+  u64 *part; /* per thread: 4 sums */
+} scr_job;
+
+static void sc_round_range(void *vctx, size_t a, size_t b, int tid) {
+  scr_job *J = (scr_job *)vctx;
+  u64 acc[4][4];
+  memset(acc, 0, sizeof acc);
+  for (size_t s = a; s < b; s++) {
+    u64 f0[FC_SC_TABLES][4], d[FC_SC_TABLES][4];
+    for (int i = 0; i < J->k; i++) {
+      if (J->fold) {
+        const u64 *p = J->src[i] + 16 * s;
+        u64 t[4];
+        fsub(&FR, t, p + 4, p);
+        fmul(&FR, t, t, J->r);
+        fadd(&FR, f0[i], p, t);
+        fsub(&FR, t, p + 12, p + 8);
+        fmul(&FR, t, t, J->r);
+        fadd(&FR, d[i], p + 8, t); /* f1 for now */
+        memcpy(J->dst[i] + 8 * s, f0[i], 32);
+        memcpy(J->dst[i] + 8 * s + 4, d[i], 32);
+      } else {
+        memcpy(f0[i], J->src[i] + 8 * s, 32);
+        memcpy(d[i], J->src[i] + 8 * s + 4, 32);
+      }
+      fsub(&FR, d[i], d[i], f0[i]);
+    }
+    u64 v[FC_SC_TABLES][4];
+    for (int i = 0; i < J->k; i++) memcpy(v[i], f0[i], 32);
+    for (int x = 0; x < 4; x++) {
+      if (x)
+        for (int i = 0; i < J->k; i++) fadd(&FR, v[i], v[i], d[i]);
+      for (int t = 0; t < J->n_terms; t++) {
+        u64 p[4];
+        memcpy(p, J->coeffs + 4 * t, 32);
+        for (int j = 0; j < 3; j++) {
+          const int ix = J->tt[3 * t + j];
+          if (ix >= 0) fmul(&FR, p, p, v[ix]);
+        }
+        fadd(&FR, acc[x], acc[x], p);
+      }
+    }
+  }
+  memcpy(J->part + 16 * tid, acc, sizeof acc);
+}
+
+static void sc_sums(scr_job *J, size_t pairs, int T, u64 e[4][4]) {
+  J->part = (u64 *)calloc((size_t)T * 16, 8);
+  par_for(pairs, T, sc_round_range, J);
+  memset(e, 0, 128);
+  for (int t = 0; t < T; t++)
+    for (int x = 0; x < 4; x++) fadd(&FR, e[x], e[x], J->part + 16 * t + 4 * x);
+  free(J->part);
+}
+
+int fc_sumcheck_prove(const uint64_t *const *tables, int n_tables, unsigned nv, const uint64_t claimed[4],
+                      int n_terms, const uint64_t *term_coeffs, const int *term_tables, const uint8_t *prefix,
+                      size_t prefix_len, int threads, uint64_t *rounds_out, uint64_t final_out[4],
+                      uint64_t *challenges_out) {
+  if (n_tables < 0 || n_tables > FC_SC_TABLES || nv > 40) return 1;
+  for (int t = 0; t < 3 * n_terms; t++)
+    if (term_tables[t] >= n_tables) return 1;
+  const int T = threads < 1 ? 1 : (threads > FC_MAX_THREADS ? FC_MAX_THREADS : threads);
+  const size_t n = (size_t)1 << nv;
+  u64 *buf[2][FC_SC_TABLES];
+  for (int i = 0; i < n_tables; i++) {
+    buf[0][i] = (u64 *)malloc((n / 2 + 1) * 32);
+    buf[1][i] = (u64 *)malloc((n / 4 + 1) * 32);
+  }
+  tr_t tr;
+  tr_init(&tr);
+  if (prefix_len) tr_put(&tr, prefix, prefix_len);
+  u64 cur[4], r[4] = {0, 0, 0, 0}, xs[4][4];
+  memcpy(cur, claimed, 32);
+  for (int i = 0; i < 4; i++) fr_u64(xs[i], (u64)i);
+  const u64 *src[FC_SC_TABLES];
+  for (int i = 0; i < n_tables; i++) src[i] = tables[i];
+  int st = 0, pp = 0;
+  for (unsigned rnd = 0; rnd < nv; rnd++) {
+    scr_job J = {{0}, {0}, n_tables, rnd > 0, r, n_terms, term_coeffs, term_tables, NULL};
+    for (int i = 0; i < n_tables; i++) {
+      J.src[i] = src[i];
+      J.dst[i] = buf[pp][i];
+    }
+    u64 e[4][4], coeffs[4][4], g0[4], g1[4], sum[4];
+    sc_sums(&J, n >> (rnd + 1), T, e);
+    if (rnd > 0) {
+      for (int i = 0; i < n_tables; i++) src[i] = buf[pp][i];
+      pp ^= 1;
+    }
+    lagrange_points(&xs[0][0], &e[0][0], 4, &coeffs[0][0]); /* src/sumcheck.rs:201-206 */
+    horner(&coeffs[0][0], 4, xs[0], g0);
+    horner(&coeffs[0][0], 4, xs[1], g1);
+    fadd(&FR, sum, g0, g1);
+    if (!eq4(sum, cur)) { st = 6; break; } /* src/sumcheck.rs:80-84 */
+    memcpy(rounds_out + 16 * rnd, coeffs, 128);
+    char lab[64];
+    snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd); /* :90-96 */
+    tr_label(&tr, lab);
+    for (int i = 0; i < 4; i++) tr_fr(&tr, coeffs[i]);
+    snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
+    tr_challenge(&tr, lab, r);
+    if (challenges_out) memcpy(challenges_out + 4 * rnd, r, 32);
+    horner(&coeffs[0][0], 4, r, cur);
+  }
+  if (!st) { /* bind the last variable; final = the composition at the bound values (:104) */
+    u64 vals[FC_SC_TABLES][4];
+    for (int i = 0; i < n_tables; i++) {
+      if (nv == 0) {
+        memcpy(vals[i], src[i], 32);
+      } else {
+        u64 t[4];
+        fsub(&FR, t, src[i] + 4, src[i]);
+        fmul(&FR, t, t, r);
+        fadd(&FR, vals[i], src[i], t);
+      }
+    }
+    u64 acc[4] = {0, 0, 0, 0};
+    for (int t = 0; t < n_terms; t++) {
+      u64 p[4];
+      memcpy(p, term_coeffs + 4 * t, 32);
+      for (int j = 0; j < 3; j++)
+        if (term_tables[3 * t + j] >= 0) fmul(&FR, p, p, vals[term_tables[3 * t + j]]);
+      fadd(&FR, acc, acc, p);
+    }
+    memcpy(final_out, acc, 32);
+  }
+  tr_free(&tr);
+  for (int i = 0; i < n_tables; i++) {
+    free(buf[0][i]);
+    free(buf[1][i]);
+  }
+  return st;
+}
+
+/* sum over the hypercube of the composition (the honest claim of fc_sumcheck_prove) */
+typedef struct {
+  const u64 *const *tabs;
+  int n_terms;
+  const u64 *coeffs;
+  const int *tt;
+  u64 *part;
+} csum_job;
+static void csum_range(void *vctx, size_t a, size_t b, int tid) {
+  csum_job *J = (csum_job *)vctx;
+  u64 acc[4] = {0, 0, 0, 0};
+  for (size_t s = a; s < b; s++)
+    for (int t = 0; t < J->n_terms; t++) {
+      u64 p[4];
+      memcpy(p, J->coeffs + 4 * t, 32);
+      for (int j = 0; j < 3; j++)
+        if (J->tt[3 * t + j] >= 0) fmul(&FR, p, p, J->tabs[J->tt[3 * t + j]] + 4 * s);
+      fadd(&FR, acc, acc, p);
+    }
+  memcpy(J->part + 4 * tid, acc, 32);
+}
+
+void fc_composition_sum(const uint64_t *const *tables, unsigned nv, int n_terms, const uint64_t *term_coeffs,
+                        const int *term_tables, int threads, uint64_t out[4]) {
+  const int T = threads < 1 ? 1 : (threads > FC_MAX_THREADS ? FC_MAX_THREADS : threads);
+  csum_job J = {tables, n_terms, term_coeffs, term_tables, (u64 *)calloc((size_t)T * 4, 8)};
+  par_for((size_t)1 << nv, T, csum_range, &J);
+  u64 s[4] = {0, 0, 0, 0};
+  for (int t = 0; t < T; t++) fadd(&FR, s, s, J.part + 4 * t);
+  memcpy(out, s, 32);
+  free(J.part);
+}

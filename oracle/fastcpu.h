@@ -33,6 +33,18 @@ int fc_twist_prove(const uint64_t *lagrange, const uint64_t *bary_w, size_t N, s
                    const uint64_t *addr, const uint64_t *val, const uint8_t *is_write, size_t n_ops,
                    int threads, orc_proof *out);
 
+/* SumCheck::prove (src/sumcheck.rs:56-110) for the composition sum_t c_t prod_j T[tt[3t+j]]
+ * (tt = -1 for unused slots, <= 4 tables of 2^nv Montgomery Fr) with O(N)-per-round table folds
+ * on `threads` host threads; transcript = prefix bytes then the rounds.  Same outputs and status
+ * (0, 1 bad arguments, 6 round check failed) as orc_sumcheck_prove. */
+int fc_sumcheck_prove(const uint64_t *const *tables, int n_tables, unsigned nv, const uint64_t claimed[4],
+                      int n_terms, const uint64_t *term_coeffs, const int *term_tables, const uint8_t *prefix,
+                      size_t prefix_len, int threads, uint64_t *rounds_out, uint64_t final_out[4],
+                      uint64_t *challenges_out);
+/* sum over {0,1}^nv of that composition (the honest claimed sum) */
+void fc_composition_sum(const uint64_t *const *tables, unsigned nv, int n_terms, const uint64_t *term_coeffs,
+                        const int *term_tables, int threads, uint64_t out[4]);
+
 #ifdef __cplusplus
 }
 #endif

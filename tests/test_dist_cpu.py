@@ -67,6 +67,7 @@ def _comm_body(rank, world):
 
     comm = ts.Comm.torch()
     assert (comm.rank, comm.size) == (rank, world)
+    assert comm.info() == {"rank": rank, "size": world, "seen_size": world, "kind": "callback"}
     got = comm.allgather(bytes([rank + 1]) * 96)  # one partial G1 point's worth per rank
     assert got == b"".join(bytes([r + 1]) * 96 for r in range(world))
     got = comm.allgather(bytes(range(rank * 8, rank * 8 + 8)))

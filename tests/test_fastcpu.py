@@ -57,3 +57,42 @@ def test_bary_weights_identity():
         ell = ell * (x - j) % po.R_MOD
     s = sum(wj * pow(x - j, -1, po.R_MOD) for j, wj in enumerate(w)) % po.R_MOD
     assert ell * s % po.R_MOD == 1
+
+
+SC_COMPOSITIONS = {
+    "abc": [(1, [0, 1, 2])],
+    "mixed": [(3, [0, 1, 2]), (po.R_MOD - 5, [1]), (7, [0, 0]), (11, [])],
+    "twist_like": [(1, [0, 1]), (po.R_MOD - 1, [2, 2, 1]), (2, [2])],
+    "cube": [(5, [1, 1, 1]), (9, [3])],
+}
+
+
+def _rand_tables(k, nv, seed):
+    rng = np.random.default_rng(seed)
+    return [co.fr_array([int.from_bytes(rng.bytes(32), "little") % po.R_MOD for _ in range(1 << nv)])
+            for _ in range(k)]
+
+
+@pytest.mark.parametrize("name", list(SC_COMPOSITIONS))
+@pytest.mark.parametrize("nv,threads", [(0, 1), (1, 2), (3, 3), (6, 4), (8, 5)])
+def test_fast_sumcheck_matches_reference_algorithm(name, nv, threads):
+    """fc_sumcheck_prove (table folds, O(N) per round) == orc_sumcheck_prove (the reference's
+    closure sum-check, src/sumcheck.rs:56-110, O(N n) per hypercube point) with the transcript
+    prefix of a caller."""
+    terms = SC_COMPOSITIONS[name]
+    tabs = _rand_tables(4, nv, seed=nv * 13 + len(name))
+    claim = co.fast_composition_sum(tabs, nv, terms, threads)
+    want = co.sumcheck_prove(tabs, nv, claim, terms, prefix=b"prefix")
+    got = co.fast_sumcheck_prove(tabs, nv, claim, terms, prefix=b"prefix", threads=threads)
+    assert want[0] == got[0] == 0
+    for a, b in zip(want[1:], got[1:]):
+        assert np.array_equal(a, b)
+
+
+def test_fast_sumcheck_wrong_claim_and_bad_table():
+    tabs = _rand_tables(3, 4, seed=1)
+    terms = SC_COMPOSITIONS["twist_like"]
+    claim = co.fast_composition_sum(tabs, 4, terms, 2)
+    assert co.fast_sumcheck_prove(tabs, 4, claim + 1, terms, threads=2)[0] == 6
+    assert co.sumcheck_prove(tabs, 4, claim + 1, terms)[0] == 6
+    assert co.fast_sumcheck_prove(tabs, 4, claim, [(1, [3])], threads=2)[0] == 1

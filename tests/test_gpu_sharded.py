@@ -167,12 +167,49 @@ def test_setup_params_shard_splits_the_srs():
             for i in range(8)] == full[:8]
 
 
+@pytest.mark.parametrize("L,n_total,size", [(18, 1 << 20, 2), (18, 1 << 20, 8), (10, 3000, 4), (6, 200, 8)])
+def test_msm_sharded_equals_unsharded(L, n_total, size):
+    """The C2 MSM at N ranks (tns_msm_sharded): each rank commits its coefficient slice against its
+    own SRS share (setup_params_shard), the 96-byte partials are allgathered; every rank returns
+    the unsharded KZGCommitment::commit (src/commitments.rs:162-180)."""
+    sc = ts.fr_rand_batch(bytes([7] * 32), n_total)
+    sc[5] = 0  # a zero scalar and a ragged tail
+    pp = params(L)
+    want = ts.msm_resident(pp.commitment_params, ts.DeviceBuffer(pp.commitment_params.srs.ctx, sc), n_total)
+
+    def body(r, comm, ctx):
+        sp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+        first, count = ts.shard_slice(n_total, r, size)
+        held_first, held = sp.commitment_params.srs.share()
+        assert held_first <= first and first + count <= held_first + held
+        d = ts.DeviceBuffer(ctx, sc[first:first + count] if count else np.zeros((1, 4), dtype=np.uint64))
+        return ts.msm_sharded_resident(sp.commitment_params, comm, d, count, n_total), comm.info()
+    got, errs = run_ranks(size, body)
+    assert errs == [None] * size
+    for r, (g, info) in enumerate(got):
+        assert np.array_equal(g, want)
+        assert info == {"rank": r, "size": size, "seen_size": size, "kind": "callback"}
+
+
+def test_msm_sharded_rejects_wrong_slice():
+    L, size, n_total = 8, 2, 512
+    sc = ts.fr_rand_batch(bytes([7] * 32), n_total)
+
+    def body(r, comm, ctx):
+        sp, _ = ts.setup_params_shard(L, r, size, ctx=ctx)
+        d = ts.DeviceBuffer(ctx, sc[:100])
+        return ts.msm_sharded_resident(sp.commitment_params, comm, d, 100, n_total)
+    _, errs = run_ranks(size, body)
+    assert all(isinstance(e, ts.InvalidParameters) for e in errs)
+
+
 def test_rccl_communicator_one_rank():
     L = 6
     addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
     want = ts.Twist(params(L)).prove_soa(addr, val, isw)
     ctx = ts.Context(0)
     comm = ts.Comm.rccl(ctx, 0, 1, ts.Comm.unique_id())
+    assert comm.info() == {"rank": 0, "size": 1, "seen_size": 1, "kind": "rccl"}  # ncclCommCount
     pp, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
     assert ts.Twist(pp).prove_sharded(comm, addr, val, isw, len(addr)) == want
 
