@@ -666,7 +666,8 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   // is more than one pass -- the accumulation reads no keys (C4: k_accumulate 9.10 -> 8.8 ms).
   const char *pke = getenv("TNS_BS_PACK"), *voe = getenv("TNS_BS_VO");
   J.vo = npass >= 2 && !(voe && voe[0] == '0');
-  J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32;
+  // (unpack_value reads the window index from the low wb bits of the last pass's L key bits: L >= wb)
+  J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 && bits[npass - 1] >= J.wb;
   for (int p = 0, rest = keybits - bits[npass - 1]; p < npass - 1; p++) {
     bits[p] = (rest + (npass - 2 - p)) / (npass - 1 - p);
     rest -= bits[p];
@@ -683,7 +684,9 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
     for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= BS_MAXBITS;
     if (ok)
       for (int p = 0; p < npass; p++) bits[p] = v[p];
-    if (ok) J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32;
+    if (ok)
+      J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 &&
+             bits[npass - 1] >= J.wb;
   }
   J.ibits = ibits;
   J.shared = shared;

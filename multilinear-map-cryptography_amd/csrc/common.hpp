@@ -304,6 +304,7 @@ class HostUpload {
     hipEvent_t ev = nullptr;
   };
   void run();
+  void run_items();
   Ctx *c_;
   std::vector<Item> items_;
   std::thread th_;

@@ -56,6 +56,23 @@ static char *stage_ring(Ctx *c) {
 }
 
 void HostUpload::run() {
+  // runs on its own thread: nothing may escape it (std::terminate would take down a process that
+  // has initialised the GPU); a failure is recorded in err_ and surfaces in wait() as a status
+  try {
+    run_items();
+  } catch (const std::bad_alloc &) {
+    std::lock_guard<std::mutex> lk(mu_);
+    err_ = hipErrorOutOfMemory;
+    done_ = true;
+  } catch (...) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (err_ == hipSuccess) err_ = hipErrorUnknown;
+    done_ = true;
+  }
+  cv_.notify_all();
+}
+
+void HostUpload::run_items() {
   hipError_t err = hipSetDevice(c_->device);
   for (size_t k = 0; k < items_.size() && err == hipSuccess; k++) {
     Item &it = items_[k];
@@ -72,8 +89,7 @@ void HostUpload::run() {
       const size_t nch = (it.bytes + kChunk - 1) / kChunk;
       std::vector<hipError_t> werr(kWorkers, hipSuccess);
       std::vector<std::thread> ws;
-      for (int w = 0; w < kWorkers && (size_t)w < nch; w++)
-        ws.emplace_back([&, w]() {
+      auto body = [&](int w) {
           hipError_t e = hipSetDevice(c_->device);
           int use = 0;
           for (size_t ch = (size_t)w; ch < nch && e == hipSuccess; ch += kWorkers, use ^= 1) {
@@ -87,7 +103,12 @@ void HostUpload::run() {
             if (e == hipSuccess) e = hipEventRecord(c_->stage_ev[slot], c_->copy);
           }
           werr[w] = e;
-        });
+      };
+      try {
+        for (int w = 0; w < kWorkers && (size_t)w < nch; w++) ws.emplace_back(body, w);
+      } catch (...) {  // a worker that could not start: its chunks go on this thread
+        for (int w = (int)ws.size(); w < kWorkers && (size_t)w < nch; w++) body(w);
+      }
       for (auto &t : ws) t.join();
       for (hipError_t e : werr)
         if (e != hipSuccess) err = e;
