@@ -126,6 +126,12 @@ int tns_srs_set_tau(tns_srs *srs, const uint64_t tau[4]);
  * proof of that size; part of setup, not of proving.  TNS_ERR_INVALID_PARAMETERS when
  * the SRS has no tau or N is not a power of two. */
 int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n);
+/* The same basis built from g1_powers[0..n) ALONE, for an SRS without tau (src/utils.rs:61, :107
+ * mark tau test-only): a transposed remainder tree over the nodes' subproduct tree, ~1.5 n log^2 n
+ * variable-base scalar multiplications on the device (tfree.hip; a one-time setup per (SRS, n) --
+ * measured cost in DESIGN.md).  Cached in the SRS: Twist/Shout::prove then take the Lagrange route
+ * on this SRS too.  n a power of two, g1_powers[0..n) held (unsharded). */
+int tns_srs_prepare_lagrange_from_powers(tns_ctx *ctx, tns_srs *srs, size_t n);
 /* Copy that basis ([L_j(tau)]G, j < n; built if needed) to host memory (affine uint64_t[8]
  * each): setup artefact for host-side provers (the CPU baseline of bench.py). */
 int tns_srs_lagrange_download(tns_ctx *ctx, tns_srs *srs, size_t n, uint64_t *g1_affine_out);

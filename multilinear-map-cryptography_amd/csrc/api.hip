@@ -528,10 +528,19 @@ int tns_srs_prepare_lagrange(tns_ctx *ctx, tns_srs *srs, size_t n) {
   });
 }
 
+int tns_srs_prepare_lagrange_from_powers(tns_ctx *ctx, tns_srs *srs, size_t n) {
+  return guarded([&]() {
+    CtxScope g(&ctx->c);
+    (void)lagrange_basis_from_powers_dev(&ctx->c, srs->s, n);
+    return TNS_OK;
+  });
+}
+
 int tns_srs_lagrange_download(tns_ctx *ctx, tns_srs *srs, size_t n, uint64_t *g1_affine_out) {
   return guarded([&]() {
     CtxScope g(&ctx->c);
-    if (!srs->s.has_tau) throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS has no tau");
+    if (!srs->s.has_tau && !srs->s.lagrange.count(std::make_tuple(n, (size_t)0, n)))
+      throw Error(TNS_ERR_INVALID_PARAMETERS, "SRS has no tau (and no basis prepared from its powers)");
     if (n == 0 || (n & (n - 1))) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lagrange basis size must be a power of two");
     const bool saved = ctx->c.lagrange_commit;
     ctx->c.lagrange_commit = true;

@@ -533,6 +533,11 @@ void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cn
 // quotient values for an opening AT the node j0 (value y_j0), unsharded
 void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q);
 bool fr_is_node(const Fr &x, size_t N);
+// barycentric weights w_j = (-1)^(N-1-j) / (j! (N-1-j)!) of the nodes [first, first + cnt) (cached)
+const Fr *bary_weights_dev(Ctx *c, size_t N, size_t first, size_t cnt);
+// tfree.hip: the Lagrange basis [L_j(tau)]G, j < N, from g1_powers[0..N) alone (no tau); cached in
+// srs.lagrange under (N, 0, N) like the tau-derived one
+const LagrangeBasis *lagrange_basis_from_powers_dev(Ctx *c, const Srs &srs, size_t N);
 
 // comm.cpp: the exchange steps of a sharded proof
 struct Comm {

@@ -274,6 +274,8 @@ static const Fr *bary_weights(Ctx *c, size_t N, size_t first, size_t cnt) {
   return w;
 }
 
+const Fr *bary_weights_dev(Ctx *c, size_t N, size_t first, size_t cnt) { return bary_weights(c, N, first, cnt); }
+
 bool fr_is_node(const Fr &x, size_t N) {
   Fr k = from_mont(x);
   for (int i = 2; i < 8; i++)
@@ -325,12 +327,12 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
 static Fr fr_shift(const Fr &x, size_t first) { return sub(x, from_u64<FrCfg>((uint64_t)first)); }
 
 const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t first, size_t cnt) {
-  if (!c->lagrange_commit || !srs.has_tau || N == 0) return nullptr;
+  if (!c->lagrange_commit || N == 0) return nullptr;
   if (first + cnt > N || cnt == 0) throw Error(TNS_ERR_INVALID_PARAMETERS, "node slice outside 0..N-1");
-  if (fr_is_node(srs.tau, N)) return nullptr;
   const auto key = std::make_tuple(N, first, cnt);
   auto it = srs.lagrange.find(key);
-  if (it != srs.lagrange.end()) return it->second;
+  if (it != srs.lagrange.end()) return it->second;  // also a basis built from g1_powers alone (tfree.hip)
+  if (!srs.has_tau || fr_is_node(srs.tau, N)) return nullptr;
   const Fr *w = bary_weights(c, N, first, cnt);
   // ell(tau) over all N nodes
   DevBuf ellb;

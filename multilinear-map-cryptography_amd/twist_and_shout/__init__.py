@@ -213,6 +213,12 @@ class Srs:
         first proof of that size."""
         _check(N.load().tns_srs_prepare_lagrange(self.ctx.handle, self.handle, n))
 
+    def prepare_lagrange_from_powers(self, n: int):
+        """Build the Lagrange basis for n = 2^k nodes from g1_powers alone (no tau needed): a
+        one-time setup (tns_srs_prepare_lagrange_from_powers) after which provers on this SRS take
+        the Lagrange route."""
+        _check(N.load().tns_srs_prepare_lagrange_from_powers(self.ctx.handle, self.handle, n))
+
     def lagrange_points(self, n: int) -> np.ndarray:
         """The Lagrange basis [L_j(tau)]G of the nodes 0..n-1 (affine limbs, host copy)."""
         out = np.zeros((n, 8), dtype=np.uint64)
@@ -261,6 +267,19 @@ class CommitmentParams:
         xs = from_mont(limbs[:, :4], P_MOD)
         ys = from_mont(limbs[:, 4:], P_MOD)
         return [None if (x == 0 and y == 0) else (x, y) for x, y in zip(xs, ys)]
+
+    @classmethod
+    def from_g1_limbs(cls, limbs: np.ndarray, device: int = 0, tau=None) -> "CommitmentParams":
+        """Upload g1_powers given as affine Montgomery limbs (n x 8 uint64, identity = zeros), e.g. an
+        Srs.download(): an SRS without tau unless one is given."""
+        ctx = Context.get(device)
+        arr = np.ascontiguousarray(limbs, dtype=np.uint64).reshape(-1, 8)
+        h = C.c_void_p()
+        _check(N.load().tns_srs_upload(ctx.handle, N.p64(arr), len(arr), C.byref(h)))
+        srs = Srs(ctx, h)
+        if tau is not None:
+            srs.set_tau(tau)
+        return cls(srs, tau)
 
     @classmethod
     def from_g1_powers(cls, g1_powers: Sequence[G1Affine], device: int = 0, tau=None) -> "CommitmentParams":

@@ -84,6 +84,7 @@ SIGNATURES = [
     ("tns_srs_set_tau", C.c_int, [C.c_void_p, U64P]),
     ("tns_srs_prepare_lagrange", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("tns_srs_lagrange_download", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, U64P]),
+    ("tns_srs_prepare_lagrange_from_powers", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("tns_ctx_set_commit_basis", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_ctx_set_msm_tables", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_ctx_set_msm_sort", C.c_int, [C.c_void_p, C.c_int]),
