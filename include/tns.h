@@ -141,7 +141,14 @@ int tns_srs_lagrange_download(tns_ctx *ctx, tns_srs *srs, size_t n, uint64_t *g1
 int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange);
 /* MSM over a fixed base (SRS, Lagrange basis): on != 0 (default) uses the base's
  * window-shifted table (built once, W copies of the points) so that every window shares
- * one bucket set; 0 forces the per-window bucket layout.  Same results. */
+ * one bucket set; 0 forces the per-window bucket layout.  Same results.
+ * MSM window tables (memory contract): a table is built the first time an MSM of >= 2^16 SRS
+ * points / >= 2^12 Lagrange-basis points runs with tables on, and lives as long as its SRS:
+ * W * n * 64 bytes for n points, W = ceil(255 / c) with the cost model's window c (C4's 2^24-node
+ * basis: c = 22, W = 12, 12.9 GB; C2's 2^20 + 1 SRS points: c = 20, W = 13, 0.87 GB).  If the
+ * device cannot hold it, the MSM runs without it (per-window buckets: same result, slower) and
+ * nothing is cached -- no error is returned for a table.  Setting 0 here before the first MSM
+ * keeps every table from being built. */
 int tns_ctx_set_msm_tables(tns_ctx *ctx, int on);
 /* The MSM's bucket order: rocprim != 0 uses a digit array + rocPRIM radix sort instead of the
  * fused digit/counting sort (default; TNS_MSM_SORT=cub at context creation does the same).

@@ -504,6 +504,8 @@ BucketOrder bucket_sort_finish(BucketSortJob &J);
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
+// the same, or nullptr when the table does not fit in device memory (TNS_ERR_OOM)
+FixedBase *fixed_base_try_build(Ctx *c, const G1Affine *points, size_t n);
 // the SRS's window table, built on first use by an MSM of >= 2^16 points (nullptr below)
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n);
 

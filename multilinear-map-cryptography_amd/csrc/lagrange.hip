@@ -355,7 +355,7 @@ const LagrangeBasis *lagrange_basis_dev(Ctx *c, const Srs &srs, size_t N, size_t
   try {
     G1Affine *pts = (G1Affine *)b->points.ensure(sizeof(G1Affine) * cnt);
     fixed_base_mul_dev(c, sc, cnt, pts);  // synchronises
-    if (cnt >= ((size_t)1 << 12)) b->fb = fixed_base_build_dev(c, pts, cnt);
+    if (cnt >= ((size_t)1 << 12)) b->fb = fixed_base_try_build(c, pts, cnt);
   } catch (...) {
     delete b;
     throw;

@@ -639,10 +639,22 @@ FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n) {
   return fb;
 }
 
+// the window table if the device has room for it: on an allocation failure the MSMs over these
+// points run without one (per-window buckets, same results) and nothing is cached
+FixedBase *fixed_base_try_build(Ctx *c, const G1Affine *points, size_t n) {
+  try {
+    return fixed_base_build_dev(c, points, n);
+  } catch (const Error &e) {
+    if (e.code != TNS_ERR_OOM) throw;
+    (void)hipGetLastError();  // clear the failed allocation's sticky status
+    return nullptr;
+  }
+}
+
 const FixedBase *srs_fixed_base(Ctx *c, const Srs &srs, size_t n) {
   if (n < ((size_t)1 << 16) || !c->msm_tables) return nullptr;
   if (srs.held < n) return nullptr;  // a shard's table covers its held points (tns_msm_sharded)
-  if (!srs.fb) srs.fb = fixed_base_build_dev(c, srs.points.as<G1Affine>(), srs.held);
+  if (!srs.fb) srs.fb = fixed_base_try_build(c, srs.points.as<G1Affine>(), srs.held);
   return srs.fb;
 }
 

@@ -336,7 +336,7 @@ const LagrangeBasis *lagrange_basis_from_powers_dev(Ctx *c, const Srs &srs, size
       xyzz_to_affine_batch_dev(c, H, N, pts, (Fq *)pre.ensure(sizeof(Fq) * N));
       TNS_HIP(hipStreamSynchronize(st));
     }
-    if (N >= ((size_t)1 << 12)) basis->fb = fixed_base_build_dev(c, pts, N);
+    if (N >= ((size_t)1 << 12)) basis->fb = fixed_base_try_build(c, pts, N);
     TNS_HIP(hipStreamSynchronize(st));
   } catch (...) {
     delete basis;
