@@ -1012,11 +1012,14 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   int v_chunks = v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? upload_chunks() : 1;
   const size_t v_per = (n_ops + v_chunks - 1) / std::max(v_chunks, 1);
   if (v_per) v_chunks = (int)((n_ops + v_per - 1) / v_per);  // chunks actually formed
+  uint32_t *dar32 = nullptr;
   if (kind == hipMemcpyHostToDevice) {
     uint64_t *dar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
     uint8_t *dfl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
     if (n_ops) {
-      up_a = upload.add(dar, addr, 8 * n_ops);
+      // the addresses cross PCIe as u32 when they fit (memory sizes < 2^32: 64 MB fewer at 2^24 ops)
+      dar32 = (uint32_t *)c->prove_ws[11].ensure(4 * n_ops);
+      up_a = upload.add_narrow(dar32, dar, addr, n_ops);
       up_f = upload.add(dfl, is_write, n_ops);
       for (int k = 0; k < v_chunks; k++) {  // item ids up_v, up_v + 1, ...
         const int id = upload.add(V + (size_t)k * v_per, value + 4 * (size_t)k * v_per,
@@ -1055,7 +1058,10 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   unsigned *a_bits = (unsigned *)c->prove_ws[9].ensure(sizeof(unsigned));
   ScalarSource src_a;
   src_a.prep = [=, &upload](hipStream_t s) {
-    if (up_a >= 0) upload.wait(up_a, s);
+    if (up_a >= 0) {
+      upload.wait(up_a, s);
+      if (upload.narrowed(up_a)) widen_u32_dev(s, dar32, n_ops, const_cast<uint64_t *>(ar));
+    }
     u64_tables_dev(s, ar, n_ops, L, A, nullptr, a_bits);
   };
   src_a.canon_bits = a_bits;
@@ -1167,10 +1173,12 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   const bool t_late = kind == hipMemcpyHostToDevice && n_entries > 0;
   int up_i = -1, up_t = -1;
   const uint64_t *ir = indices;
+  uint32_t *dir32 = nullptr;
   if (kind == hipMemcpyHostToDevice) {
     if (n_lookups) {
       uint64_t *dir = (uint64_t *)d_idx_raw.ensure(8 * n_lookups);
-      up_i = upload.add(dir, indices, 8 * n_lookups);
+      dir32 = (uint32_t *)c->prove_ws[11].ensure(4 * n_lookups);  // u32 over PCIe when they fit
+      up_i = upload.add_narrow(dir32, dir, indices, n_lookups);
       ir = dir;
     }
     if (t_late) up_t = upload.add(TB, entries, sizeof(Fr) * n_entries);
@@ -1181,7 +1189,10 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
   unsigned hbad = 0;
   if (n_lookups) {
-    if (up_i >= 0) upload.wait(up_i, st);
+    if (up_i >= 0) {
+      upload.wait(up_i, st);
+      if (upload.narrowed(up_i)) widen_u32_dev(st, dir32, n_lookups, const_cast<uint64_t *>(ir));
+    }
     unsigned *bad = (unsigned *)d_bad.ensure(sizeof(unsigned));
     TNS_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), st));
     k_max_index_check<<<grid_for(n_lookups, 256), 256, 0, st>>>(ir, n_lookups, n_entries_total, bad);

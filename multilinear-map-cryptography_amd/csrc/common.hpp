@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -292,6 +293,11 @@ class HostUpload {
   HostUpload(const HostUpload &) = delete;
   HostUpload &operator=(const HostUpload &) = delete;
   int add(void *dst, const void *src, size_t bytes);
+  // n u64 values (trace addresses, lookup indices) sent as u32 into dst32 when every value fits
+  // (half the PCIe bytes), else as they are into dst64; narrowed(item) says which, once wait(item)
+  // has returned
+  int add_narrow(uint32_t *dst32, uint64_t *dst64, const uint64_t *src, size_t n);
+  bool narrowed(int item);
   void start();
   void wait(int item, hipStream_t s);
   void wait_all(hipStream_t s);
@@ -302,9 +308,12 @@ class HostUpload {
     const void *src = nullptr;
     size_t bytes = 0;
     hipEvent_t ev = nullptr;
+    bool narrow = false, narrowed = false;
+    void *dst_wide = nullptr;
   };
   void run();
   void run_items();
+  hipError_t transfer(char *ring, void *dst, const void *src, size_t bytes, bool narrow, std::atomic<bool> *fits);
   Ctx *c_;
   std::vector<Item> items_;
   std::thread th_;
@@ -381,6 +390,8 @@ void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 // u64 entries [0, n_in) zero-padded to n: Montgomery form (mont), canonical form (canon,
 // optional) and the largest bit length (*bits, zeroed here) in one pass on stream s
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits);
+// out[i] = in[i] widened to u64 (addresses / indices that crossed PCIe as u32), on stream s
+void widen_u32_dev(hipStream_t s, const uint32_t *in, size_t n, uint64_t *out);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
 // fb_off: the points are entries [fb_off, fb_off + n) of the set fb was built for

@@ -106,6 +106,18 @@ __global__ void __launch_bounds__(256) k_u64_tables(const uint64_t *__restrict__
   }
   block_atomic_max2(b, 0u, bits, nullptr);
 }
+__global__ void __launch_bounds__(256) k_widen_u32(const uint32_t *__restrict__ in, size_t n,
+                                                   uint64_t *__restrict__ out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = in[i];
+}
+
+void widen_u32_dev(hipStream_t s, const uint32_t *in, size_t n, uint64_t *out) {
+  if (!n) return;
+  k_widen_u32<<<grid_for(n, 256, 4096), 256, 0, s>>>(in, n, out);
+  TNS_LAUNCH_CHECK();
+}
+
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits) {
   TNS_HIP(hipMemsetAsync(bits, 0, sizeof(unsigned), s));
   if (!n) return;

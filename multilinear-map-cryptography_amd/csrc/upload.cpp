@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -48,6 +49,18 @@ int HostUpload::add(void *dst, const void *src, size_t bytes) {
   return (int)items_.size() - 1;
 }
 
+int HostUpload::add_narrow(uint32_t *dst32, uint64_t *dst64, const uint64_t *src, size_t n) {
+  const int id = add(dst32, src, 8 * n);
+  items_[id].narrow = true;
+  items_[id].dst_wide = dst64;
+  return id;
+}
+
+bool HostUpload::narrowed(int item) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return items_[item].narrowed;
+}
+
 // the staging ring: kSlots chunks of pinned memory and one event per slot (its last DMA)
 static char *stage_ring(Ctx *c) {
   if (!c->stage_ev[0])
@@ -72,12 +85,64 @@ void HostUpload::run() {
   cv_.notify_all();
 }
 
+// One transfer through the pinned ring: kWorkers threads each fill their two slots in turn and DMA
+// them on the copy stream.  narrow: the source is u64 values and each chunk lands as u32 (half
+// the PCIe bytes); *fits turns false if a value needs more than 32 bits (the bytes sent are then
+// wrong and the caller sends the u64 array instead).
+hipError_t HostUpload::transfer(char *ring, void *dst, const void *src, size_t bytes, bool narrow,
+                                std::atomic<bool> *fits) {
+  const size_t unit = narrow ? 8 : 1, per = narrow ? kChunk / 4 : kChunk;  // source units per chunk
+  const size_t total = bytes / unit, nch = (total + per - 1) / per;
+  std::vector<hipError_t> werr(kWorkers, hipSuccess);
+  std::vector<std::thread> ws;
+  auto body = [&](int w) {
+    hipError_t e = hipSetDevice(c_->device);
+    int use = 0;
+    for (size_t ch = (size_t)w; ch < nch && e == hipSuccess; ch += kWorkers, use ^= 1) {
+      const int slot = 2 * w + use;
+      char *buf = ring + (size_t)slot * kChunk;
+      const size_t off = ch * per, cnt = std::min(per, total - off);
+      e = hipEventSynchronize(c_->stage_ev[slot]);  // the slot's previous DMA is done
+      if (e != hipSuccess) break;
+      size_t len = cnt;
+      if (narrow) {
+        const uint64_t *in = (const uint64_t *)src + off;
+        uint32_t *o = (uint32_t *)buf;
+        uint64_t any = 0;
+        for (size_t i = 0; i < cnt; i++) {
+          any |= in[i];
+          o[i] = (uint32_t)in[i];
+        }
+        if (any >> 32) fits->store(false, std::memory_order_relaxed);
+        len = 4 * cnt;
+        e = hipMemcpyAsync((uint32_t *)dst + off, buf, len, hipMemcpyHostToDevice, c_->copy);
+      } else {
+        std::memcpy(buf, (const char *)src + off, len);
+        e = hipMemcpyAsync((char *)dst + off, buf, len, hipMemcpyHostToDevice, c_->copy);
+      }
+      if (e == hipSuccess) e = hipEventRecord(c_->stage_ev[slot], c_->copy);
+    }
+    werr[w] = e;
+  };
+  try {
+    for (int w = 0; w < kWorkers && (size_t)w < nch; w++) ws.emplace_back(body, w);
+  } catch (...) {  // a worker that could not start: its chunks go on this thread
+    for (int w = (int)ws.size(); w < kWorkers && (size_t)w < nch; w++) body(w);
+  }
+  for (auto &t : ws) t.join();
+  for (hipError_t e : werr)
+    if (e != hipSuccess) return e;
+  return hipSuccess;
+}
+
 void HostUpload::run_items() {
   hipError_t err = hipSetDevice(c_->device);
   for (size_t k = 0; k < items_.size() && err == hipSuccess; k++) {
     Item &it = items_[k];
-    if (it.bytes < kDirect) {
-      if (it.bytes) err = hipMemcpyAsync(it.dst, it.src, it.bytes, hipMemcpyHostToDevice, c_->copy);
+    bool narrowed = false;
+    if (it.bytes < kDirect) {  // (narrow items: small arrays go over as they are)
+      if (it.bytes) err = hipMemcpyAsync(it.narrow ? it.dst_wide : it.dst, it.src, it.bytes, hipMemcpyHostToDevice,
+                                         c_->copy);
     } else {
       char *ring = nullptr;
       try {
@@ -86,36 +151,19 @@ void HostUpload::run_items() {
         err = hipErrorOutOfMemory;
         break;
       }
-      const size_t nch = (it.bytes + kChunk - 1) / kChunk;
-      std::vector<hipError_t> werr(kWorkers, hipSuccess);
-      std::vector<std::thread> ws;
-      auto body = [&](int w) {
-          hipError_t e = hipSetDevice(c_->device);
-          int use = 0;
-          for (size_t ch = (size_t)w; ch < nch && e == hipSuccess; ch += kWorkers, use ^= 1) {
-            const int slot = 2 * w + use;
-            char *buf = ring + (size_t)slot * kChunk;
-            const size_t off = ch * kChunk, len = std::min(kChunk, it.bytes - off);
-            e = hipEventSynchronize(c_->stage_ev[slot]);  // the slot's previous DMA is done
-            if (e != hipSuccess) break;
-            std::memcpy(buf, (const char *)it.src + off, len);
-            e = hipMemcpyAsync((char *)it.dst + off, buf, len, hipMemcpyHostToDevice, c_->copy);
-            if (e == hipSuccess) e = hipEventRecord(c_->stage_ev[slot], c_->copy);
-          }
-          werr[w] = e;
-      };
-      try {
-        for (int w = 0; w < kWorkers && (size_t)w < nch; w++) ws.emplace_back(body, w);
-      } catch (...) {  // a worker that could not start: its chunks go on this thread
-        for (int w = (int)ws.size(); w < kWorkers && (size_t)w < nch; w++) body(w);
+      if (it.narrow) {
+        std::atomic<bool> fits(true);
+        err = transfer(ring, it.dst, it.src, it.bytes, true, &fits);
+        narrowed = fits.load();
+        if (err == hipSuccess && !narrowed) err = transfer(ring, it.dst_wide, it.src, it.bytes, false, nullptr);
+      } else {
+        err = transfer(ring, it.dst, it.src, it.bytes, false, nullptr);
       }
-      for (auto &t : ws) t.join();
-      for (hipError_t e : werr)
-        if (e != hipSuccess) err = e;
     }
     if (err == hipSuccess) err = hipEventRecord(it.ev, c_->copy);
     {
       std::lock_guard<std::mutex> lk(mu_);
+      it.narrowed = narrowed;
       queued_ = (int)k + 1;
       if (err != hipSuccess) err_ = err;
     }

@@ -100,3 +100,31 @@ def test_c5_srs_shards_partition_g1_powers():
                 srs.points_at([first - 1])
         del pp, srs
     assert nxt == n
+
+
+@pytest.mark.parametrize("wide", [False, True])
+def test_dropin_address_narrowing(wide):
+    """The drop-in prover sends u64 addresses over PCIe as u32 when every address fits (HostUpload
+    add_narrow, widened on the device) and as u64 otherwise; both equal the device-resident proof.
+    2^20 ops (8 MB of addresses: the staged path)."""
+    L = 18
+    n = 1 << 20
+    pp, _ = params(L)
+    addr, val, isw = ts.bench_trace(1 << L, n)
+    if wide:
+        addr = addr.copy()
+        addr[n // 3] = (1 << 40) + 5  # one address past 32 bits: the u64 fallback
+    ctx = pp.commitment_params.srs.ctx
+    d = [ts.DeviceBuffer(ctx, x) for x in (addr, val, isw)]
+    want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
+    assert ts.Twist(pp).prove_soa(addr, val, isw) == want
+
+
+def test_dropin_shout_index_narrowing():
+    L, T, M = 18, 1 << 20, 1 << 20
+    pp, _ = params(L)
+    entries = ts.fr_from_u64_array(np.arange(T, dtype=np.uint64) * 3)
+    idx = (np.arange(M, dtype=np.uint64) * 7) % T
+    ctx = pp.commitment_params.srs.ctx
+    raw = ts.shout_prove_resident(pp, ts.DeviceBuffer(ctx, entries), T, ts.DeviceBuffer(ctx, idx), M)
+    assert ts.Shout(pp).prove_arrays(entries, idx) == ts.shout_proof_from_raw(raw)
