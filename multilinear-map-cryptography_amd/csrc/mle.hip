@@ -110,7 +110,9 @@ Fr mle_evaluate_dev(Ctx *c, const Fr *evals, unsigned nv, const Fr *point_host) 
 // FOLD:   tables in[] have 4P entries; bind r into out[] (2P entries), then sum round values.
 // !FOLD:  tables in[] have 2P entries (first round), just sum.
 // Block partial sums (4 Fr: X = 0..3) -> partials[blockIdx.x * 4 + X].
-template <bool FOLD, bool TERMS>
+// SKIP1: the sum at X = 1 is not formed (the host takes it as claim - g(0): from round 1 on the
+// round polynomial's g(0) + g(1) equals the previous round's g(r) identically, src/sumcheck.rs:80-84)
+template <bool FOLD, bool TERMS, bool SKIP1 = false>
 __global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms terms, size_t P, Fr r,
                                                   Fr *__restrict__ partials) {
   __shared__ Fr lds[4 * 16];
@@ -141,6 +143,7 @@ __global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms ter
       for (int i = 0; i < MAX_SC_TABLES; i++)
         if (i < k) d[i] = sub(f1[i], f0[i]);
       for (int x = 0; x < 4; x++) {
+        if (SKIP1 && x == 1) continue;
         Fr vx[MAX_SC_TABLES];
 #pragma unroll
         for (int i = 0; i < MAX_SC_TABLES; i++) {
@@ -459,7 +462,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
         if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
       } else {
         if (has_terms)
-          k_sc_round<true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
+          k_sc_round<true, true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
         else
           k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
         // src now holds the freshly folded 2P-entry tables
@@ -480,6 +483,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
       TNS_LAUNCH_CHECK();
       TNS_HIP(hipMemcpyAsync(e, sums_dev, sizeof e, hipMemcpyDeviceToHost, c->stream));
       TNS_HIP(hipStreamSynchronize(c->stream));
+      if (rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
     }
     Fr coeffs[4];
     interpolate4_host(e, coeffs);  // lagrange_interpolate of 4 points (src/sumcheck.rs:201-206)
