@@ -222,6 +222,9 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ bstar
 #ifndef TNS_ACC_MINB
 #define TNS_ACC_MINB 1
 #endif
+// KEYS (a template parameter, so the default values-only sort's variant carries none of the key
+// path's registers): the sort left a key per entry (else the runs come from the bucket starts)
+template <bool KEYS>
 __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals,
                                                     const uint32_t *__restrict__ valid_p,
@@ -230,20 +233,21 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
                                                     HeadTail *__restrict__ ht, size_t nchunks, int ks,
                                                     int acc_k, const uint32_t *__restrict__ bstart, size_t nb,
                                                     uint2 *__restrict__ cbk) {
-  const size_t valid = *valid_p;
+  // entry positions are 32-bit (a sort holds < 2^31 entries, msm_launch_sort): one VGPR each
+  const uint32_t valid = *valid_p;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
-    const size_t a = t * acc_k;
+    const uint32_t a = (uint32_t)t * (uint32_t)acc_k;
     if (a >= valid) continue;
-    const size_t b = a + acc_k < valid ? a + acc_k : valid;
+    const uint32_t b = a + acc_k < valid ? a + acc_k : valid;
     // a run is a head (it began before this chunk) iff it is the chunk's first run and entry
     // a - 1 has its bucket, a tail (it goes on after the chunk) iff it is the last run and entry
     // b has its bucket: two key loads per chunk instead of the run's bounds at every flush.
     // Flushed sums stay in the lazy domain [0, 2M): the fixup and the reduction add them lazily.
     uint32_t cur, after;
     bool head_run;
-    size_t nxt = 0;  // (no keys) the start of the bucket after `cur`
-    if (keys) {
+    uint32_t nxt = 0;  // (no keys) the start of the bucket after `cur`
+    if (KEYS) {
       cur = keys[a] >> ks;
       head_run = a > 0 && (keys[a - 1] >> ks) == cur;
       after = b < valid ? keys[b] >> ks : 0xffffffffu;
@@ -260,10 +264,10 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
     uint32_t v1 = vals[a], v2 = a + 1 < b ? vals[a + 1] : 0u;
     G1Affine q1 = load_point(pts, v1 & TNS_ACC_PTMASK);
 #endif
-    for (size_t p = a;; p++) {
-      const bool brk = keys ? p >= b || (keys[p] >> ks) != cur : p >= b || p >= nxt;
+    for (uint32_t p = a;; p++) {
+      const bool brk = KEYS ? p >= b || (keys[p] >> ks) != cur : p >= b || p >= nxt;
       if (brk) {  // flush the run of bucket `cur`
-        const bool tail = keys ? after == cur : nxt > b;
+        const bool tail = KEYS ? after == cur : nxt > b;
         if (first && head_run) ht[t].head = acc;
         else if (p >= b && tail) ht[t].tail = acc;
         else buckets[cur] = acc;
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
           break;
         }
         first = false;
-        if (keys) {
+        if (KEYS) {
           cur = keys[p] >> ks;
         } else {
           do {  // skip empty buckets
@@ -733,7 +737,7 @@ static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
   }
   static const int bpc = [] {  // resident blocks of 256 threads per CU (VGPR-bound: 3)
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_accumulate, 256, 0) != hipSuccess || b < 1) b = 3;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_accumulate<false>, 256, 0) != hipSuccess || b < 1) b = 3;
     return b;
   }();
   const size_t slots = (size_t)ctx->num_cu * bpc * 256;
@@ -894,9 +898,9 @@ static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * J.n);  // 96 B per (scalar, point) pair
     const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
     uint2 *cbk = (uint2 *)ln.ws[16].ensure(sizeof(uint2) * J.nchunks);
-    k_accumulate<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets,
-                                                                     ht, J.nchunks, J.ks, J.acc_k, J.bstart, J.P.nb,
-                                                                     cbk);
+    auto acc = J.keys2 ? k_accumulate<true> : k_accumulate<false>;
+    acc<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets, ht, J.nchunks,
+                                                            J.ks, J.acc_k, J.bstart, J.P.nb, cbk);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));

@@ -14,9 +14,12 @@ typedef unsigned u32;
 #define MADC(s, c) \
   asm volatile("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc" : "+v"(s), "+v"(c) : "v"(a), "v"(b) : "vcc")
 #define ADD(x) asm volatile("v_add_u32_e32 %0, %1, %0" : "+v"(x) : "v"(a))
+#define MULLO(x) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(x) : "v"(a))
+#define MOV2(x, y) asm volatile("v_mov_b32_e32 %0, %1" : "=v"(x) : "v"(y))
 
 // kind 0: 8 independent mads; 1: 8 independent mad+addc; 2: one dependent mad chain (8 per iter);
-// 3: one dependent mad+addc chain; 4: 8 independent full-rate adds; 5: 2 chains of mad+addc
+// 3: one dependent mad+addc chain; 4: 8 independent full-rate adds; 5: 2 chains of mad+addc;
+// 6: 8 independent v_mul_lo_u32 (the Montgomery quotient digit m = t * INV)
 template <int KIND>
 __global__ void __launch_bounds__(64) k_bench(u32 *x, int iters) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -31,6 +34,7 @@ __global__ void __launch_bounds__(64) k_bench(u32 *x, int iters) {
     if (KIND == 3) { MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); MADC(s0, c0); }
     if (KIND == 4) { ADD(y0); ADD(y1); ADD(y2); ADD(y3); ADD(y4); ADD(y5); ADD(y6); ADD(y7); }
     if (KIND == 5) { MADC(s0, c0); MADC(s1, c1); MADC(s0, c0); MADC(s1, c1); MADC(s0, c0); MADC(s1, c1); MADC(s0, c0); MADC(s1, c1); }
+    if (KIND == 6) { MULLO(y0); MULLO(y1); MULLO(y2); MULLO(y3); MULLO(y4); MULLO(y5); MULLO(y6); MULLO(y7); }
   }
   x[i] = (u32)(s0 ^ s1 ^ s2 ^ s3 ^ s4 ^ s5 ^ s6 ^ s7) + c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7 +
          (y0 ^ y1 ^ y2 ^ y3 ^ y4 ^ y5 ^ y6 ^ y7);
@@ -57,10 +61,10 @@ int main() {
   hipMalloc(&d, sizeof(u32) * (256 * 4 * 8 * 64 + 64));
   hipMemset(d, 0x5a, sizeof(u32) * (256 * 4 * 8 * 64 + 64));
   const int it = 4000;
-  printf("waves/SIMD | add x8 | mad x8 | mad+addc x8 | mad chain | mad+addc chain | 2 mad+addc chains   (G lane-ops/s)\n");
+  printf("waves/SIMD | add x8 | mad x8 | mad+addc x8 | mad chain | mad+addc chain | 2 mad+addc chains | mul_lo x8  (G lane-ops/s)\n");
   for (int w : {1, 2, 3, 4, 6, 8}) {
-    printf("%d | %.0f | %.0f | %.0f | %.0f | %.0f | %.0f\n", w, run<4>(d, w, it), run<0>(d, w, it), run<1>(d, w, it),
-           run<2>(d, w, it), run<3>(d, w, it), run<5>(d, w, it));
+    printf("%d | %.0f | %.0f | %.0f | %.0f | %.0f | %.0f | %.0f\n", w, run<4>(d, w, it), run<0>(d, w, it), run<1>(d, w, it),
+           run<2>(d, w, it), run<3>(d, w, it), run<5>(d, w, it), run<6>(d, w, it));
   }
   return 0;
 }
