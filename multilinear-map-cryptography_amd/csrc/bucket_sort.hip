@@ -37,6 +37,9 @@ constexpr int BS_BLOCK = TNS_BS_BLOCK;  // 4 waves: fits the slots k_accumulate 
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
 constexpr int BS_TILE = 8192;  // entries per tile at most (LDS staging: 64 KiB)
+// the tile of sorts that run beside an MSM accumulation (BucketSortJob::corun): 8 entries per
+// thread, so the scatter kernels stay within the registers the accumulation leaves free
+constexpr int BS_CORUN_TILE = 2048;
 // per-pass tile sizes (template parameter TILE of the scatter kernels): 8192 or 4096 entries
 constexpr int BS_SCALARS = 4;  // scalars a pass-1 thread loads ahead
 
@@ -357,12 +360,16 @@ struct Pass1Plan {
   void (*count)(DigitArgs, int, int, size_t, uint32_t *);
   void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, int, uint32_t *, uint32_t *);
   int spt;
+  bool corun;  // a plan for sorts that run beside an accumulation (BucketSortJob::corun)
 };
-#define TNS_P1(T, C, W, SPT) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT}
-static const Pass1Plan kPass1Plans[] = {TNS_P1(BS_TILE, 22, 12, 3), TNS_P1(BS_TILE, 20, 13, 3), TNS_P1(BS_TILE, 19, 14, 3),
-                                        TNS_P1(BS_TILE, 17, 15, 3), TNS_P1(BS_TILE, 16, 2, 16), TNS_P1(BS_TILE, 12, 2, 16),
-                                        // half tiles (half the LDS: twice the blocks per CU)
-                                        TNS_P1(4096, 22, 12, 2), TNS_P1(4096, 20, 13, 2)};
+#define TNS_P1(T, C, W, SPT, CO) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT, CO}
+static const Pass1Plan kPass1Plans[] = {
+    TNS_P1(BS_TILE, 22, 12, 3, false), TNS_P1(BS_TILE, 20, 13, 3, false), TNS_P1(BS_TILE, 19, 14, 3, false),
+    TNS_P1(BS_TILE, 17, 15, 3, false), TNS_P1(BS_TILE, 16, 2, 16, false), TNS_P1(BS_TILE, 12, 2, 16, false),
+    // half tiles (half the LDS: twice the blocks per CU)
+    TNS_P1(4096, 22, 12, 2, false), TNS_P1(4096, 20, 13, 2, false),
+    // co-running sorts (BucketSortJob::corun): 2048-entry tiles, at most one scalar per thread
+    TNS_P1(BS_CORUN_TILE, 22, 12, 1, true), TNS_P1(BS_CORUN_TILE, 20, 13, 1, true)};
 #undef TNS_P1
 
 // bins of pass 1 -> segment starts; seg[nbins] = total = number of entries (also *valid)
@@ -635,7 +642,9 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   const size_t E = (size_t)W * n;
   if (E >= ((size_t)1 << 32)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one bucket sort");
   if (W > BS_TILE) throw Error(TNS_ERR_COMMITMENT, "too many MSM windows");
+  const bool corun = J.corun;  // the caller's choice survives the reset
   J = BucketSortJob();
+  J.corun = corun;
   J.ln = &ln;
   J.valid = valid;
   J.E = E;
@@ -711,11 +720,11 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
-  const int tile1 = W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
+  const int tile1 = J.corun ? BS_CORUN_TILE : W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
   const Pass1Plan *ct = nullptr;
   if (!getenv("TNS_BS_RUNTIME_PASS1"))  // (A/B: the runtime-plan kernels)
     for (const Pass1Plan &p : kPass1Plans)
-      if (p.tile == tile1 && p.c == c && p.W == W) ct = &p;
+      if (p.tile == tile1 && p.c == c && p.W == W && p.corun == J.corun) ct = &p;
   A.spb = (size_t)tile1 / W;
   if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
   const size_t T1 = (n + A.spb - 1) / A.spb;
@@ -724,7 +733,8 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   uint32_t **seg = J.seg;
   seg[0] = (uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1));
   seg[1] = (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1));
-  const size_t max_tiles = (E + 4095) / 4096 + (max_seg >> bits[npass - 1]) + 1;  // smallest tile: 4096
+  const size_t tmin = J.corun ? BS_CORUN_TILE : 4096;  // the smallest pass tile
+  const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> bits[npass - 1]) + 1;
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
@@ -764,7 +774,7 @@ void bucket_sort_passes(BucketSortJob &J) {
     J.p = p;
     J.nb = 1 << bits[p];
     J.shift -= bits[p];
-    int tile = pass_tile(p);
+    int tile = J.corun ? BS_CORUN_TILE : pass_tile(p);
     if (!tile) tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
     J.tile = tile;
     // In the last pass most segments fit one tile and rank locally; only segments of >= 2
@@ -821,13 +831,19 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
   uint32_t *counts = J.counts, *offs = J.offs;
   if (!ident) {
     if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
-    if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    if (tile == BS_CORUN_TILE)
+      k_bs_count<BS_CORUN_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    else if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
   }
   {
-    auto *kern = tile == 4096 ? (pk == 0   ? k_bs_scatter<4096, 0>
+    auto *kern = tile == BS_CORUN_TILE ? (pk == 0   ? k_bs_scatter<BS_CORUN_TILE, 0>
+                                          : pk == 1 ? k_bs_scatter<BS_CORUN_TILE, 1>
+                                          : pk == 2 ? k_bs_scatter<BS_CORUN_TILE, 2>
+                                                    : k_bs_scatter<BS_CORUN_TILE, 3>)
+               : tile == 4096 ? (pk == 0   ? k_bs_scatter<4096, 0>
                                  : pk == 1 ? k_bs_scatter<4096, 1>
                                  : pk == 2 ? k_bs_scatter<4096, 2>
                                            : k_bs_scatter<4096, 3>)

@@ -502,6 +502,10 @@ struct BucketSortJob {
   // bits, the sign and the point index i (ibits bits) -- and the last pass reads that word and
   // writes the accumulation's values only (no keys: runs come from the bucket starts)
   bool pk = false, vo = false, shared = false;  // vo: the last pass writes values only
+  // set before bucket_sort_begin: the sort runs beside another lane's accumulation, so it uses the
+  // small-register kernels (2048-entry pass tiles, one scalar per pass-1 thread) that fit in the
+  // 80 registers per lane k_accumulate's three waves per SIMD leave free
+  bool corun = false;
   int ibits = 0, p = 0;
   uint32_t stride = 0;
   int kf[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key format pass p writes (bucket_sort.hip KF_*)

@@ -1124,6 +1124,10 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     }
     TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
     (void)hipEventDestroy(sorted);
+    // lane 1's sort runs beside that accumulation: the small-register sort kernels, which fit in
+    // what its three waves per SIMD leave free (TNS_SORT_CORUN=0: the full-size kernels, A/B)
+    const char *cr = getenv("TNS_SORT_CORUN");
+    jb.bs.corun = !(cr && cr[0] == '0') && ja.sorted;
     msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
   } else {
     // both lanes' passes are queued before either lane's host wait (the last pass's readback),

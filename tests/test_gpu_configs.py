@@ -189,3 +189,24 @@ def test_twist_dropin_chunked_value_commitment(chunks, monkeypatch):
         d = [ts.DeviceBuffer(ctx, x) for x in (addr, v, isw)]
         want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
         assert ts.Twist(pp).prove_soa(addr, v, isw) == want
+
+
+@pytest.mark.parametrize("corun", ["1", "0"])
+@pytest.mark.parametrize("L", [14, 18])
+def test_twist_staggered_corun_sort_same_proof(L, corun, monkeypatch):
+    """The staggered two-lane MSM schedule (TNS_MSM_STAGGER=1, read at context creation): lane 1's
+    bucket sort runs beside lane 0's accumulation with the small-register kernels (2048-entry
+    tiles, BucketSortJob::corun), or with the full-size ones (TNS_SORT_CORUN=0).  Same proof as
+    the default schedule, Twist and Shout."""
+    pp, _ = params(L)
+    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
+    want = ts.Twist(pp).prove_soa(addr, val, isw)
+    entries = ts.to_mont([i * i + 3 for i in range(1 << 12)])
+    idx = (np.arange(1 << (L + 1), dtype=np.uint64) * 7) % (1 << 12)
+    want_s = ts.Shout(pp).prove_arrays(entries, idx)
+    monkeypatch.setenv("TNS_MSM_STAGGER", "1")
+    monkeypatch.setenv("TNS_SORT_CORUN", corun)
+    ctx = ts.Context(0)
+    pp2, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
+    assert ts.Twist(pp2).prove_soa(addr, val, isw) == want
+    assert ts.Shout(pp2).prove_arrays(entries, idx) == want_s
