@@ -1013,6 +1013,11 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   const size_t v_per = (n_ops + v_chunks - 1) / std::max(v_chunks, 1);
   if (v_per) v_chunks = (int)((n_ops + v_per - 1) / v_per);  // chunks actually formed
   uint32_t *dar32 = nullptr;
+  // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
+  // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
+  unsigned lr = 0;
+  while ((1 << lr) < m.size) lr++;
+  const bool flag_bytes = sumcheck_folds_take_flag_bytes(nv - lr);
   if (kind == hipMemcpyHostToDevice) {
     uint64_t *dar = (uint64_t *)d_addr_raw.ensure(8 * (n_ops ? n_ops : 1));
     uint8_t *dfl = (uint8_t *)d_flags.ensure(n_ops ? n_ops : 1);
@@ -1020,12 +1025,15 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
       // the addresses cross PCIe as u32 when they fit (memory sizes < 2^32: 64 MB fewer at 2^24 ops)
       dar32 = (uint32_t *)c->prove_ws[11].ensure(4 * n_ops);
       up_a = upload.add_narrow(dar32, dar, addr, n_ops);
-      up_f = upload.add(dfl, is_write, n_ops);
+      // flags read by the folds only (after both commitments) go last: their copy then runs under
+      // the last value chunk's MSM instead of ahead of the values
+      if (!flag_bytes) up_f = upload.add(dfl, is_write, n_ops);
       for (int k = 0; k < v_chunks; k++) {  // item ids up_v, up_v + 1, ...
         const int id = upload.add(V + (size_t)k * v_per, value + 4 * (size_t)k * v_per,
                                   sizeof(Fr) * std::min(v_per, n_ops - (size_t)k * v_per));
         if (k == 0) up_v = id;
       }
+      if (flag_bytes) up_f = upload.add(dfl, is_write, n_ops);
       upload.start();
     }
     ar = dar;
@@ -1034,11 +1042,6 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     TNS_HIP(hipMemcpyAsync(V, value, sizeof(Fr) * n_ops, kind, st));
   }
   if (L > n_ops) fr_fill_zero_dev(c, V + n_ops, L - n_ops);
-  // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
-  // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
-  unsigned lr = 0;
-  while ((1 << lr) < m.size) lr++;
-  const bool flag_bytes = sumcheck_folds_take_flag_bytes(nv - lr);
   if (!flag_bytes) {
     O = (Fr *)d_o.ensure(sizeof(Fr) * L);
     if (up_f >= 0) upload.wait(up_f, st);

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -250,7 +251,7 @@ struct Ctx {
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
   hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)
   PinnedBuf stage;             // their pinned staging ring (upload.cpp, built on first use)
-  hipEvent_t stage_ev[16] = {};
+  hipEvent_t stage_ev[32] = {};  // upload.cpp's staging ring: one event per slot
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)
   MsmLane lanes[2];     // lanes[0].stream == stream; lanes[1] has its own stream
   DevBuf prove_ws[12];  // resident trace / evaluation / quotient vectors of Twist/Shout::prove
@@ -308,14 +309,31 @@ class HostUpload {
     const void *src = nullptr;
     size_t bytes = 0;
     hipEvent_t ev = nullptr;
-    bool narrow = false, narrowed = false;
+    bool narrow = false, narrowed = false, done = false;
     void *dst_wide = nullptr;
   };
+  struct Job {  // one chunk of one item (or a whole small item: direct)
+    int item;
+    size_t off, cnt;  // source units: bytes, or u64 values for a narrow item
+    bool direct;
+  };
+  struct ItemState {  // worker-side progress of an item
+    std::atomic<size_t> left{0};
+    std::atomic<bool> fits{true};
+  };
   void run();
-  void run_items();
-  hipError_t transfer(char *ring, void *dst, const void *src, size_t bytes, bool narrow, std::atomic<bool> *fits);
+  void run_jobs();
+  void work(int w, char *ring, std::atomic<size_t> &next, std::atomic<bool> &stop);
+  hipError_t do_job(const Job &j, char *ring, int w, int &use);
+  hipError_t finish_item(int k, char *ring, int w, int &use);
+  hipError_t stage(char *ring, int w, int &use, void *dst, const void *src, size_t bytes);
+  void mark_first();
+  std::chrono::steady_clock::time_point t_start_, t_first_;
+  std::atomic<bool> first_marked_{false};
   Ctx *c_;
   std::vector<Item> items_;
+  std::vector<Job> jobs_;
+  std::unique_ptr<ItemState[]> state_;
   std::thread th_;
   std::mutex mu_;
   std::condition_variable cv_;
