@@ -503,6 +503,33 @@ __global__ void __launch_bounds__(64) k_reduce_level(const G1Xyzz *__restrict__ 
   }
 }
 
+// second level over the first level's (T, S) (sets x g1, groups of L1): per group h
+//   u_h = sum T_g,  S2_h = sum S_g,  W_h = sum_j j S_{h L1 + j}  (the running sum added BEFORE
+//   each element: no negation), and V_h = u_h + 2^lg0 W_h (lg0 doublings: L0 = 2^lg0).
+// Then sum_g T_g + L0 sum_g g S_g = sum_h V_h + L0 L1 sum_h h S2_h, so the masked sums run over
+// g1 / L1 groups with weight L0 L1.  Short chains (3 L1 additions + lg0 doublings) instead of the
+// masked sums' ~nbits/2-fold re-reading of every S_g: C2's masked sums took 0.32 of its 2.3 ms.
+__global__ void __launch_bounds__(64) k_reduce_level2(const G1Xyzz *__restrict__ T, const G1Xyzz *__restrict__ S,
+                                                      int sets, size_t g1, int L1, int lg0,
+                                                      G1Xyzz *__restrict__ V, G1Xyzz *__restrict__ S2) {
+  const size_t groups = g1 / L1;
+  for (size_t id = blockIdx.x * (size_t)blockDim.x + threadIdx.x; id < (size_t)sets * groups;
+       id += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = id / groups, h = id % groups;
+    const size_t base = r * g1 + h * L1;
+    G1Xyzz run = G1Xyzz::inf(), w = G1Xyzz::inf(), u = G1Xyzz::inf();
+    for (int j = L1 - 1; j >= 0; j--) {
+      w = xyzz_add_lazy(w, run);  // + sum_{k > j} S_k: S_k counted k times in the end
+      run = xyzz_add_lazy(run, S[base + j]);
+      u = xyzz_add_lazy(u, T[base + j]);
+    }
+    w = xyzz_canon(w);
+    for (int q = 0; q < lg0; q++) w = xyzz_dbl(w);
+    V[id] = xyzz_add_lazy(u, w);
+    S2[id] = run;
+  }
+}
+
 // parts[(r specs + s) nch + ch], nch = g / (2 CH) chunks of CH items per spec s of set r:
 //   s < nbits: the groups gi with bit s set, enumerated directly (the k-th is k with a one
 //   inserted at bit s: every lane of a wave adds, no masked-off lanes);
@@ -953,17 +980,32 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
   // (C2, 2^20 points: 2.73 -> 2.65 ms); from 2^21 buckets 16 / 16 stay the fastest (2^22, 2^24)
   const bool small_sets = P.half <= ((size_t)1 << 19);
   J.L0 = (int)std::min<size_t>(ctx->red_l > 0 ? ctx->red_l : (small_sets ? 4 : RED_L), P.half / 2);
-  const size_t g = P.half / J.L0;
+  const size_t g1 = P.half / J.L0;
+  // second level (k_reduce_level2) when the first leaves many groups: L1 = 4 (TNS_RED_L1; 0 = off)
+  int L1 = g1 >= ((size_t)1 << 13) ? 4 : 0;
+  if (const char *e = getenv("TNS_RED_L1")) L1 = std::max(0, atoi(e));
+  if (L1 && ((L1 & (L1 - 1)) || g1 / L1 < 2)) L1 = 0;  // powers of two, >= 2 groups left
+  const size_t g = L1 ? g1 / L1 : g1;
   J.nbits = 0;
   while (((size_t)1 << J.nbits) < g) J.nbits++;
   J.specs = J.nbits + 2;
   {
     TNS_PROF_ON(ctx, st, "msm_reduce", 128.0 * P.nb);
-    G1Xyzz *T = (G1Xyzz *)ln.ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * g);
-    G1Xyzz *S = T + (size_t)P.Wr * g;
-    k_reduce_level<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
+    G1Xyzz *T = (G1Xyzz *)ln.ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * (g1 + (L1 ? g : 0)));
+    G1Xyzz *S = T + (size_t)P.Wr * g1;
+    k_reduce_level<<<grid_for((size_t)P.Wr * g1, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
     TNS_LAUNCH_CHECK();
-    const int CH = (int)std::min<size_t>(ctx->red_ch > 0 ? ctx->red_ch : (small_sets ? 8 : 16), g / 2);
+    if (L1) {
+      G1Xyzz *V = S + (size_t)P.Wr * g1, *S2 = V + (size_t)P.Wr * g;
+      int lg0 = 0;
+      while ((1 << lg0) < J.L0) lg0++;
+      k_reduce_level2<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g1, L1, lg0, V, S2);
+      TNS_LAUNCH_CHECK();
+      T = V;
+      S = S2;
+      J.L0 *= L1;  // the masked sums' weight (msm_complete's doublings)
+    }
+    const int CH = (int)std::min<size_t>(ctx->red_ch > 0 ? ctx->red_ch : (small_sets || L1 ? 8 : 16), g / 2);
     const size_t nch = g / (2 * (size_t)CH);
     const size_t nparts = (size_t)P.Wr * J.specs * nch;
     G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
