@@ -20,7 +20,6 @@
 // inside one (bucket, window) run is unspecified (LDS atomics): bucket sums are group
 // elements, so the MSM result does not depend on it.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -595,12 +594,125 @@ __global__ void k_bs_bucket_starts(const uint32_t *__restrict__ seg, size_t nb, 
     out[b] = seg[b << wb];
 }
 
-template <class T>
-static void exclusive_scan(hipStream_t st, DevBuf &tmp, const T *in, T *out, size_t n) {
-  size_t bytes = 0;
-  TNS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n, st));
-  void *t = tmp.ensure(bytes);
-  TNS_HIP(hipcub::DeviceScan::ExclusiveSum(t, bytes, in, out, (int)n, st));
+// ---- exclusive scan of u32 counts (the sort's bin offsets): tiles of 4096 (256 threads x 16
+// consecutive items), reduce -> one block scanning the tile sums -> apply; a single tile is one
+// launch.  Replaces rocPRIM's look-back scan (round 3: 432 library launches per step).
+constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+
+// exclusive prefix of x over the block (NT threads); *sum = the block total.  lds: NT / 64 words
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t *lds, uint32_t &sum) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) lds[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const uint32_t v = lds[i];
+    off += i < w ? v : 0u;
+    tot += v;
+  }
+  __syncthreads();  // lds free for the caller's next scan
+  sum = tot;
+  return off + inc - x;
+}
+
+// thread's SCAN_ITEMS consecutive items of the tile (zeros past n)
+__device__ __forceinline__ void scan_load(const uint32_t *__restrict__ in, size_t n, size_t base, uint32_t (&x)[SCAN_ITEMS]) {
+  if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(in) & 15) == 0) {
+    const uint4 *p = reinterpret_cast<const uint4 *>(in + base);  // base is a multiple of 16 items
+#pragma unroll
+    for (int q = 0; q < SCAN_ITEMS / 4; q++) {
+      const uint4 v = p[q];
+      x[4 * q] = v.x;
+      x[4 * q + 1] = v.y;
+      x[4 * q + 2] = v.z;
+      x[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) x[k] = base + k < n ? in[base + k] : 0u;
+  }
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint32_t *__restrict__ in, size_t n,
+                                                              uint32_t *__restrict__ part) {
+  __shared__ uint32_t lds[SCAN_THREADS / 64];
+  uint32_t x[SCAN_ITEMS];
+  scan_load(in, n, (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS, x);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) s += x[k];
+  uint32_t tot;
+  (void)block_excl_scan<SCAN_THREADS>(s, lds, tot);
+  if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// the tile sums, scanned in place by one block
+__global__ void __launch_bounds__(1024) k_scan_parts(uint32_t *__restrict__ part, size_t np) {
+  __shared__ uint32_t lds[1024 / 64];
+  uint32_t carry = 0;
+  for (size_t b0 = 0; b0 < np; b0 += 1024) {
+    const size_t i = b0 + threadIdx.x;
+    const uint32_t x = i < np ? part[i] : 0u;
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<1024>(x, lds, tot);
+    if (i < np) part[i] = carry + pre;
+    carry += tot;
+  }
+}
+
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t *__restrict__ in, size_t n,
+                                                             const uint32_t *__restrict__ part,
+                                                             uint32_t *__restrict__ out) {
+  __shared__ uint32_t lds[SCAN_THREADS / 64];
+  const size_t base = (size_t)blockIdx.x * SCAN_TILE + (size_t)threadIdx.x * SCAN_ITEMS;
+  uint32_t x[SCAN_ITEMS];
+  scan_load(in, n, base, x);
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_ITEMS; k++) {
+    const uint32_t v = x[k];
+    x[k] = s;  // in-thread exclusive prefix
+    s += v;
+  }
+  uint32_t tot;
+  const uint32_t off = (part ? part[blockIdx.x] : 0u) + block_excl_scan<SCAN_THREADS>(s, lds, tot);
+  if (base + SCAN_ITEMS <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    uint4 *o = reinterpret_cast<uint4 *>(out + base);
+#pragma unroll
+    for (int q = 0; q < SCAN_ITEMS / 4; q++)
+      o[q] = make_uint4(off + x[4 * q], off + x[4 * q + 1], off + x[4 * q + 2], off + x[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+      if (base + k < n) out[base + k] = off + x[k];
+  }
+}
+
+// out[i] = sum_{j < i} in[j] for i < n (in and out distinct device arrays; 16-byte vector
+// loads / stores where the array is 16-byte aligned)
+static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint32_t *out, size_t n) {
+  if (!n) return;
+  const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  if (tiles == 1) {
+    k_scan_apply<<<1, SCAN_THREADS, 0, st>>>(in, n, nullptr, out);
+    TNS_LAUNCH_CHECK();
+    return;
+  }
+  uint32_t *part = (uint32_t *)tmp.ensure(sizeof(uint32_t) * tiles);
+  k_scan_reduce<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, n, part);
+  TNS_LAUNCH_CHECK();
+  k_scan_parts<<<1, 1024, 0, st>>>(part, tiles);
+  TNS_LAUNCH_CHECK();
+  k_scan_apply<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, n, part, out);
+  TNS_LAUNCH_CHECK();
 }
 
 // tile size of pass p (0-based; 8192 or 4096 entries).  TNS_BS_TILES="t0,t1,t2" overrides
