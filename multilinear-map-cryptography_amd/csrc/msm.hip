@@ -343,6 +343,10 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
     // every entry of [a, b) in one bucket: the bucket of entry a (that chunk's first) is the bucket
     // of entry b - 1 (the last chunk's last), as k_accumulate recorded them
     const bool uniform = b <= valid && cbk[a / acc_k].x == cbk[(b - 1) / acc_k].y;
+    // a wave whose 8 groups all span several buckets has nothing to sum (those sums are never
+    // read): skip its butterfly -- most of a narrow commitment's groups (the 22-bit address MSM:
+    // ~4 entries a bucket) are such, and the level ran 0.9 ms beside the value accumulation
+    if (!__any(uniform)) continue;
     G1Xyzz acc = G1Xyzz::inf();
     if (uniform) acc = level == 1 ? ht[g * FIX_FAN + j].head : below[g * FIX_FAN + j];
     for (int off = FIX_FAN / 2; off > 0; off >>= 1) {  // every lane of the wave takes part
