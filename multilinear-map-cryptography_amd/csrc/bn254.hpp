@@ -86,7 +86,11 @@ typedef Fp<FrCfg> Fr;
 typedef Fp<FqCfg> Fq;
 
 #if defined(__HIPCC__)
+#if defined(TNS_FIELD_BI)
+#include "field_bi.inc"
+#else
 #include "field_asm.inc"
+#endif
 #endif
 
 // ---------------------------------------------------------------- raw 256-bit helpers
@@ -492,6 +496,13 @@ __device__ __forceinline__ bool fq_zero_lazy(const Fq &a) {
 // constant-bus read per VALU instruction on gfx9: VCC is already one).
 template <class C, bool TWO_M>
 __device__ __forceinline__ Fp<C> const_minus_dev(const Fp<C> &a) {
+#if defined(TNS_FIELD_BI)
+  Fp<C> d;
+  unsigned br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(TWO_M ? C::M2[i] : C::M[i], a.v[i], br, &br);
+  return d;
+#endif
   Fp<C> r = a;
   const u32 *K = TWO_M ? C::M2 : C::M;
   asm("v_sub_co_u32_e32 %0, vcc, %8, %0\n\tv_subb_co_u32_e32 %1, vcc, %9, %1, vcc\n\t"
