@@ -222,7 +222,7 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
       a.prep = s->prep;
       a.late = s->late;
       a.chunks = s->chunks;
-      a.chunk_len = s->chunk_len;
+      a.chunk_off = s->chunk_off;
       a.chunk_prep = s->chunk_prep;
       a.canon = s->canon;
       a.canon_bits = s->canon_bits;
@@ -959,6 +959,24 @@ static int upload_chunks() {
   return std::max(1, std::min(64, k));
 }
 
+// The node ranges the drop-in values arrive in: k equal ranges; TNS_UPLOAD_SPLIT_LAST=1 splits
+// the last one in two halves, so the MSM left after the upload is an eighth of the vector
+// instead of a quarter -- measured equal at C4 (56.4-57.5 vs 56.4-57.9 ms per drop-in proof,
+// profiles/r04_ab_upload_split.txt: the last chunk's fixed tail dominates), so not the default.
+static std::vector<size_t> upload_chunk_offsets(size_t n, int k) {
+  std::vector<size_t> off;
+  const size_t per = (n + k - 1) / std::max(k, 1);
+  for (size_t o = 0; o < n; o += per) off.push_back(o);
+  const char *e = getenv("TNS_UPLOAD_SPLIT_LAST");
+  const bool split = e && e[0] == '1';
+  if (split && off.size() > 1) {
+    const size_t last = off.back(), len = n - last;
+    if (len >= 2) off.push_back(last + len / 2);
+  }
+  off.push_back(n);
+  return off;
+}
+
 struct SideDrain {
   Ctx *c;
   ~SideDrain() { (void)hipStreamSynchronize(c->side); }
@@ -1009,9 +1027,9 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   int up_a = -1, up_f = -1, up_v = -1;
   // the values arrive in v_chunks node ranges, each committed as it lands (TNS_UPLOAD_CHUNKS,
   // default 4; 1 = one upload, one MSM after it); padded slices (L > n_ops) keep one MSM
-  int v_chunks = v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? upload_chunks() : 1;
-  const size_t v_per = (n_ops + v_chunks - 1) / std::max(v_chunks, 1);
-  if (v_per) v_chunks = (int)((n_ops + v_per - 1) / v_per);  // chunks actually formed
+  const std::vector<size_t> v_off =
+      upload_chunk_offsets(n_ops, v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? upload_chunks() : 1);
+  const int v_chunks = std::max(1, (int)v_off.size() - 1);  // ranges actually formed
   uint32_t *dar32 = nullptr;
   // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
   // themselves (sumcheck_folds_take_flag_bytes), else it is written on the side stream
@@ -1029,8 +1047,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
       // the last value chunk's MSM instead of ahead of the values
       if (!flag_bytes) up_f = upload.add(dfl, is_write, n_ops);
       for (int k = 0; k < v_chunks; k++) {  // item ids up_v, up_v + 1, ...
-        const int id = upload.add(V + (size_t)k * v_per, value + 4 * (size_t)k * v_per,
-                                  sizeof(Fr) * std::min(v_per, n_ops - (size_t)k * v_per));
+        const int id = upload.add(V + v_off[k], value + 4 * v_off[k], sizeof(Fr) * (v_off[k + 1] - v_off[k]));
         if (k == 0) up_v = id;
       }
       if (flag_bytes) up_f = upload.add(dfl, is_write, n_ops);
@@ -1063,7 +1080,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   src_a.prep = [=, &upload](hipStream_t s) {
     if (up_a >= 0) {
       upload.wait(up_a, s);
-      if (upload.narrowed(up_a)) widen_u32_dev(s, dar32, n_ops, const_cast<uint64_t *>(ar));
+      widen_dev(s, dar32, upload.narrow_width(up_a), n_ops, const_cast<uint64_t *>(ar));
     }
     u64_tables_dev(s, ar, n_ops, L, A, nullptr, a_bits);
   };
@@ -1092,7 +1109,7 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     src_v.late = true;
     if (v_chunks > 1 && m.size == 1) {
       src_v.chunks = v_chunks;
-      src_v.chunk_len = v_per;
+      src_v.chunk_off = v_off;
       src_v.chunk_prep = [&upload, up_v](int k, hipStream_t s) { upload.wait(up_v + k, s); };
     }
   }
@@ -1194,7 +1211,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   if (n_lookups) {
     if (up_i >= 0) {
       upload.wait(up_i, st);
-      if (upload.narrowed(up_i)) widen_u32_dev(st, dir32, n_lookups, const_cast<uint64_t *>(ir));
+      widen_dev(st, dir32, upload.narrow_width(up_i), n_lookups, const_cast<uint64_t *>(ir));
     }
     unsigned *bad = (unsigned *)d_bad.ensure(sizeof(unsigned));
     TNS_HIP(hipMemsetAsync(bad, 0, sizeof(unsigned), st));

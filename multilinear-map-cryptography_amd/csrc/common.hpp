@@ -294,11 +294,12 @@ class HostUpload {
   HostUpload(const HostUpload &) = delete;
   HostUpload &operator=(const HostUpload &) = delete;
   int add(void *dst, const void *src, size_t bytes);
-  // n u64 values (trace addresses, lookup indices) sent as u32 into dst32 when every value fits
-  // (half the PCIe bytes), else as they are into dst64; narrowed(item) says which, once wait(item)
-  // has returned
-  int add_narrow(uint32_t *dst32, uint64_t *dst64, const uint64_t *src, size_t n);
-  bool narrowed(int item);
+  // n u64 values (trace addresses, lookup indices) sent packed into `small` (4 n bytes) as 24-bit
+  // values (3 bytes each, four to three words) when every value is below 2^24, else as u32 when
+  // every value fits 32 bits, else as they are into dst64; narrow_width(item) says which (3, 4 or
+  // 8 bytes a value) once wait(item) has returned -- widen_dev expands the first two
+  int add_narrow(uint32_t *small, uint64_t *dst64, const uint64_t *src, size_t n);
+  int narrow_width(int item);
   void start();
   void wait(int item, hipStream_t s);
   void wait_all(hipStream_t s);
@@ -309,7 +310,8 @@ class HostUpload {
     const void *src = nullptr;
     size_t bytes = 0;
     hipEvent_t ev = nullptr;
-    bool narrow = false, narrowed = false, done = false;
+    bool narrow = false, done = false;
+    int width = 8;  // bytes a value crossed PCIe as (narrow items)
     void *dst_wide = nullptr;
   };
   struct Job {  // one chunk of one item (or a whole small item: direct)
@@ -319,7 +321,7 @@ class HostUpload {
   };
   struct ItemState {  // worker-side progress of an item
     std::atomic<size_t> left{0};
-    std::atomic<bool> fits{true};
+    std::atomic<bool> fits24{true}, fits32{true};
   };
   void run();
   void run_jobs();
@@ -327,6 +329,7 @@ class HostUpload {
   hipError_t do_job(const Job &j, char *ring, int w, int &use);
   hipError_t finish_item(int k, char *ring, int w, int &use);
   hipError_t stage(char *ring, int w, int &use, void *dst, const void *src, size_t bytes);
+  hipError_t stage_u32(char *ring, int w, int &use, uint32_t *dst, const uint64_t *src, size_t n);
   void mark_first();
   std::chrono::steady_clock::time_point t_start_, t_first_;
   std::atomic<bool> first_marked_{false};
@@ -410,6 +413,8 @@ void fr_fill_zero_dev(Ctx *c, Fr *p, size_t n);
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits);
 // out[i] = in[i] widened to u64 (addresses / indices that crossed PCIe as u32), on stream s
 void widen_u32_dev(hipStream_t s, const uint32_t *in, size_t n, uint64_t *out);
+// HostUpload narrow items: width 3 (packed 24-bit) or 4 (u32) -> u64 (width 8: nothing to do)
+void widen_dev(hipStream_t s, const uint32_t *in, int width, size_t n, uint64_t *out);
 
 // msm.hip (fb: optional window table of `points`, enabling the shared-bucket layout)
 // fb_off: the points are entries [fb_off, fb_off + n) of the set fb was built for
@@ -466,20 +471,20 @@ struct MsmArgs {
   // the scalars are still arriving (a host upload in flight; prep waits for it): msm_pair_dev
   // queues the other MSM whole before this one's prep
   bool late = false;
-  // late and chunks > 1: the scalars arrive in `chunks` equal node ranges (the last one ragged),
-  // chunk k ready once chunk_prep(k, stream) returns; msm_pair_dev sums one MSM per chunk as
-  // each lands (table plans use the window table at the chunk's offset), so only the last
-  // chunk's MSM follows the upload
+  // late and chunks > 1: the scalars arrive in `chunks` node ranges, chunk k = scalars
+  // [chunk_off[k], chunk_off[k + 1]), ready once chunk_prep(k, stream) returns; msm_pair_dev sums
+  // one MSM per chunk as each lands (table plans use the window table at the chunk's offset), so
+  // only the last chunk's MSM follows the upload
   int chunks = 0;
-  size_t chunk_len = 0;  // chunk k = scalars [k chunk_len, min(n, (k + 1) chunk_len))
+  std::vector<size_t> chunk_off;  // chunks + 1 offsets, increasing, chunk_off[chunks] = n
   std::function<void(int, hipStream_t)> chunk_prep;
 };
 // how one vector of commit_evals_pair gets ready (the MsmArgs fields of the same names)
 struct ScalarSource {
   std::function<void(hipStream_t)> prep;
   bool late = false;
-  int chunks = 0;                                   // (MsmArgs::chunks, chunk_len, chunk_prep)
-  size_t chunk_len = 0;
+  int chunks = 0;                                   // (MsmArgs::chunks, chunk_off, chunk_prep)
+  std::vector<size_t> chunk_off;
   std::function<void(int, hipStream_t)> chunk_prep;
   const Fr *canon = nullptr;
   const unsigned *canon_bits = nullptr;

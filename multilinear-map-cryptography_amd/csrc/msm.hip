@@ -1124,10 +1124,12 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja);
     msm_launch_reduce(ctx, ja);
     if (b.chunks > 1) {  // one MSM per uploaded chunk, each as soon as it lands
-      const size_t per = b.chunk_len;
+      if ((int)b.chunk_off.size() != b.chunks + 1 || b.chunk_off.back() != b.n)
+        throw Error(TNS_ERR_INVALID_PARAMETERS, "chunk offsets do not cover the scalars");
       G1Xyzz acc = G1Xyzz::inf();
-      for (int k = 0; k < b.chunks && (size_t)k * per < b.n; k++) {
-        const size_t off = (size_t)k * per, cnt = std::min(per, b.n - off);
+      for (int k = 0; k < b.chunks; k++) {
+        const size_t off = b.chunk_off[k], cnt = b.chunk_off[k + 1] - off;
+        if (!cnt) continue;
         MsmArgs bk{b.points + off, b.scalars + off, cnt, b.fb};
         bk.prep = [&b, k](hipStream_t s) { b.chunk_prep(k, s); };
         MsmJob jk;

@@ -118,6 +118,27 @@ void widen_u32_dev(hipStream_t s, const uint32_t *in, size_t n, uint64_t *out) {
   TNS_LAUNCH_CHECK();
 }
 
+// 24-bit values packed four to three words (upload.cpp) -> u64; one thread per group of four
+__global__ void __launch_bounds__(256) k_widen_u24(const uint32_t *__restrict__ in, size_t n,
+                                                   uint64_t *__restrict__ out) {
+  const size_t groups = (n + 3) / 4;
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < groups; g += (size_t)gridDim.x * blockDim.x) {
+    const uint32_t w0 = in[3 * g], w1 = in[3 * g + 1], w2 = in[3 * g + 2];
+    const uint64_t v[4] = {w0 & 0xffffffu, (w0 >> 24) | ((w1 & 0xffffu) << 8), (w1 >> 16) | ((w2 & 0xffu) << 16),
+                           w2 >> 8};
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (4 * g + k < n) out[4 * g + k] = v[k];
+  }
+}
+
+void widen_dev(hipStream_t s, const uint32_t *in, int width, size_t n, uint64_t *out) {
+  if (!n || width == 8) return;
+  if (width == 4) return widen_u32_dev(s, in, n, out);
+  k_widen_u24<<<grid_for((n + 3) / 4, 256, 4096), 256, 0, s>>>(in, n, out);
+  TNS_LAUNCH_CHECK();
+}
+
 void u64_tables_dev(hipStream_t s, const uint64_t *in, size_t n_in, size_t n, Fr *mont, Fr *canon, unsigned *bits) {
   TNS_HIP(hipMemsetAsync(bits, 0, sizeof(unsigned), s));
   if (!n) return;

@@ -61,16 +61,16 @@ int HostUpload::add(void *dst, const void *src, size_t bytes) {
   return (int)items_.size() - 1;
 }
 
-int HostUpload::add_narrow(uint32_t *dst32, uint64_t *dst64, const uint64_t *src, size_t n) {
-  const int id = add(dst32, src, 8 * n);
+int HostUpload::add_narrow(uint32_t *small, uint64_t *dst64, const uint64_t *src, size_t n) {
+  const int id = add(small, src, 8 * n);
   items_[id].narrow = true;
   items_[id].dst_wide = dst64;
   return id;
 }
 
-bool HostUpload::narrowed(int item) {
+int HostUpload::narrow_width(int item) {
   std::lock_guard<std::mutex> lk(mu_);
-  return items_[item].narrowed;
+  return items_[item].width;
 }
 
 // the staging ring: kSlots chunks of pinned memory and one event per slot (its last DMA)
@@ -139,8 +139,9 @@ hipError_t HostUpload::do_job(const Job &j, char *ring, int w, int &use) {
     return hipMemcpyAsync(it.narrow ? it.dst_wide : it.dst, it.src, it.bytes, hipMemcpyHostToDevice, c_->copy);
   }
   if (!it.narrow) return stage(ring, w, use, (char *)it.dst + j.off, (const char *)it.src + j.off, j.cnt);
-  // narrow: u64 values -> u32 in the slot; any value past 32 bits clears the item's fits flag (the
-  // bytes sent are then wrong, and finish_item sends the u64 array instead)
+  // narrow: u64 values -> 24-bit values packed four to three words in the slot (chunk offsets are
+  // multiples of 4 values); a value past 24 (32) bits clears the item's fits24 (fits32) flag --
+  // the bytes sent are then wrong, and finish_item sends the u32 (u64) array instead
   const int slot = w * kPerWorker + use;
   use = (use + 1) % kPerWorker;
   uint32_t *o = (uint32_t *)(ring + (size_t)slot * kChunk);
@@ -148,13 +149,40 @@ hipError_t HostUpload::do_job(const Job &j, char *ring, int w, int &use) {
   if (e != hipSuccess) return e;
   const uint64_t *in = (const uint64_t *)it.src + j.off;
   uint64_t any = 0;
-  for (size_t i = 0; i < j.cnt; i++) {
-    any |= in[i];
-    o[i] = (uint32_t)in[i];
+  const size_t q = j.cnt / 4;
+  for (size_t g = 0; g < q; g++) {
+    const uint64_t a = in[4 * g], b = in[4 * g + 1], c = in[4 * g + 2], d = in[4 * g + 3];
+    any |= a | b | c | d;
+    o[3 * g] = (uint32_t)(a & 0xffffff) | (uint32_t)(b << 24);
+    o[3 * g + 1] = (uint32_t)((b >> 8) & 0xffff) | (uint32_t)(c << 16);
+    o[3 * g + 2] = (uint32_t)((c >> 16) & 0xff) | (uint32_t)(d << 8);
   }
-  if (any >> 32) state_[j.item].fits.store(false, std::memory_order_relaxed);
+  if (j.cnt % 4) {  // the item's last values: a zero-padded group
+    uint64_t v[4] = {0, 0, 0, 0};
+    for (size_t i = 4 * q; i < j.cnt; i++) v[i - 4 * q] = in[i];
+    any |= v[0] | v[1] | v[2] | v[3];
+    o[3 * q] = (uint32_t)(v[0] & 0xffffff) | (uint32_t)(v[1] << 24);
+    o[3 * q + 1] = (uint32_t)((v[1] >> 8) & 0xffff) | (uint32_t)(v[2] << 16);
+    o[3 * q + 2] = (uint32_t)((v[2] >> 16) & 0xff) | (uint32_t)(v[3] << 8);
+  }
+  if (any >> 24) state_[j.item].fits24.store(false, std::memory_order_relaxed);
+  if (any >> 32) state_[j.item].fits32.store(false, std::memory_order_relaxed);
   mark_first();
-  e = hipMemcpyAsync((uint32_t *)it.dst + j.off, o, 4 * j.cnt, hipMemcpyHostToDevice, c_->copy);
+  const size_t words = 3 * ((j.cnt + 3) / 4);
+  e = hipMemcpyAsync((uint32_t *)it.dst + 3 * (j.off / 4), o, 4 * words, hipMemcpyHostToDevice, c_->copy);
+  if (e == hipSuccess) e = hipEventRecord(c_->stage_ev[slot], c_->copy);
+  return e;
+}
+
+// n u64 values as u32 through worker w's next ring slot (a narrow item's 32-bit fallback)
+hipError_t HostUpload::stage_u32(char *ring, int w, int &use, uint32_t *dst, const uint64_t *src, size_t n) {
+  const int slot = w * kPerWorker + use;
+  use = (use + 1) % kPerWorker;
+  uint32_t *o = (uint32_t *)(ring + (size_t)slot * kChunk);
+  hipError_t e = hipEventSynchronize(c_->stage_ev[slot]);
+  if (e != hipSuccess) return e;
+  for (size_t i = 0; i < n; i++) o[i] = (uint32_t)src[i];
+  e = hipMemcpyAsync(dst, o, 4 * n, hipMemcpyHostToDevice, c_->copy);
   if (e == hipSuccess) e = hipEventRecord(c_->stage_ev[slot], c_->copy);
   return e;
 }
@@ -165,14 +193,22 @@ hipError_t HostUpload::finish_item(int k, char *ring, int w, int &use) {
   Item &it = items_[k];
   hipError_t e = hipSuccess;
   const bool chunked = it.bytes >= kDirect;
-  const bool narrowed = it.narrow && chunked && state_[k].fits.load();
-  if (it.narrow && chunked && !narrowed)
-    for (size_t off = 0; off < it.bytes && e == hipSuccess; off += kChunk)
-      e = stage(ring, w, use, (char *)it.dst_wide + off, (const char *)it.src + off, std::min(kChunk, it.bytes - off));
+  int width = 8;
+  if (it.narrow && chunked) {
+    width = state_[k].fits24.load() ? 3 : state_[k].fits32.load() ? 4 : 8;
+    const size_t n = it.bytes / 8, per = kChunk / 4;
+    const uint64_t *src = (const uint64_t *)it.src;
+    if (width == 4)  // (rare: memories or tables past 2^24 entries)
+      for (size_t off = 0; off < n && e == hipSuccess; off += per)
+        e = stage_u32(ring, w, use, (uint32_t *)it.dst + off, src + off, std::min(per, n - off));
+    if (width == 8)
+      for (size_t off = 0; off < it.bytes && e == hipSuccess; off += kChunk)
+        e = stage(ring, w, use, (char *)it.dst_wide + off, (const char *)it.src + off, std::min(kChunk, it.bytes - off));
+  }
   if (e == hipSuccess) e = hipEventRecord(it.ev, c_->copy);
   {
     std::lock_guard<std::mutex> lk(mu_);
-    it.narrowed = narrowed;
+    it.width = width;
     it.done = true;
     while (queued_ < (int)items_.size() && items_[queued_].done) queued_++;
     if (e != hipSuccess && err_ == hipSuccess) err_ = e;

@@ -1166,6 +1166,22 @@ def twist_prove_resident(pp: ProverParams, addr: DeviceBuffer, value: DeviceBuff
     return pr
 
 
+def twist_prove_host_raw(pp: ProverParams, addr: np.ndarray, value: np.ndarray, is_write: np.ndarray) -> N.TnsProof:
+    """Twist::prove on host buffers through the C ABI (tns_twist_prove: the drop-in call a Rust
+    binding makes, PCIe included); returns the raw C proof struct -- what the Rust side receives --
+    without building the Python proof objects (Twist.prove_soa adds those)."""
+    srs = pp.commitment_params.srs
+    addr = np.ascontiguousarray(addr, dtype=np.uint64)
+    value = np.ascontiguousarray(value, dtype=np.uint64).reshape(-1, 4)
+    is_write = np.ascontiguousarray(is_write, dtype=np.uint8)
+    n = len(addr)
+    pr = N.TnsProof()
+    _check(N.load().tns_twist_prove(srs.ctx.handle, srs.handle, C.byref(pp.raw()),
+                                    N.p64(addr if n else np.zeros(1, dtype=np.uint64)), N.p64(_nonempty(value)),
+                                    N.p8(is_write if n else np.zeros(1, dtype=np.uint8)), n, C.byref(pr)))
+    return pr
+
+
 def shout_prove_resident(pp: ProverParams, entries: DeviceBuffer, n_entries: int, indices: DeviceBuffer,
                          n_lookups: int) -> N.TnsProof:
     srs = pp.commitment_params.srs

@@ -170,12 +170,16 @@ def test_twist_packed_sort_tail_same_proof(L, var, monkeypatch):
     assert a == b
 
 
-@pytest.mark.parametrize("chunks", ["1", "3", "4", "7"])
+@pytest.mark.parametrize("chunks", ["1", "3", "4", "7", "4/split", "3/split"])
 def test_twist_dropin_chunked_value_commitment(chunks, monkeypatch):
     """The drop-in prover commits the value vector chunk by chunk as its upload lands
-    (TNS_UPLOAD_CHUNKS node ranges, one MSM each, summed): full-width values take the window-table
-    plan at each chunk's offset, the bench trace's narrow values the per-window plan; both equal
-    the device-resident proof (one MSM over the whole vector)."""
+    (TNS_UPLOAD_CHUNKS node ranges, the last one split in two with TNS_UPLOAD_SPLIT_LAST=1; one
+    MSM each, summed): full-width values take the window-table plan at each chunk's offset, the
+    bench trace's narrow values the per-window plan; both equal the device-resident proof (one MSM
+    over the whole vector)."""
+    chunks, _, split = chunks.partition("/")
+    if split:
+        monkeypatch.setenv("TNS_UPLOAD_SPLIT_LAST", "1")
     L = 16
     pp, _ = params(L)
     n = 1 << (L + 2)

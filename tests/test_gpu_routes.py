@@ -102,22 +102,25 @@ def test_c5_srs_shards_partition_g1_powers():
     assert nxt == n
 
 
-@pytest.mark.parametrize("wide", [False, True])
-def test_dropin_address_narrowing(wide):
-    """The drop-in prover sends u64 addresses over PCIe as u32 when every address fits (HostUpload
-    add_narrow, widened on the device) and as u64 otherwise; both equal the device-resident proof.
-    2^20 ops (8 MB of addresses: the staged path)."""
-    L = 18
-    n = 1 << 20
+@pytest.mark.parametrize("big", [None, (1 << 28) + 3, (1 << 40) + 5, (1 << 24) - 1])
+def test_dropin_address_narrowing(big):
+    """The drop-in prover sends u64 addresses over PCIe as packed 24-bit values when every address
+    is below 2^24, as u32 when one is not but all fit 32 bits, and as u64 otherwise (HostUpload
+    add_narrow; widened on the device); every form equals the device-resident proof.  2^20 + 3 ops
+    (8 MB of addresses: the staged path, a ragged last group of the 24-bit packing)."""
+    L = 19  # max_operations 2^21: the trace pads to 2^21
+    n = (1 << 20) + 3
     pp, _ = params(L)
     addr, val, isw = ts.bench_trace(1 << L, n)
-    if wide:
+    if big is not None:
         addr = addr.copy()
-        addr[n // 3] = (1 << 40) + 5  # one address past 32 bits: the u64 fallback
+        addr[n // 3] = big  # past 24 bits: the u32 fallback; past 32 bits: u64; 2^24 - 1: still 24-bit
+        addr[n - 1] = big
     ctx = pp.commitment_params.srs.ctx
     d = [ts.DeviceBuffer(ctx, x) for x in (addr, val, isw)]
     want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
     assert ts.Twist(pp).prove_soa(addr, val, isw) == want
+    assert ts.twist_proof_from_raw(ts.twist_prove_host_raw(pp, addr, val, isw)) == want  # the bench's drop-in call
 
 
 def test_dropin_shout_index_narrowing():
