@@ -19,13 +19,16 @@
 // correlations of group vectors with scalar polynomials: small nodes directly, larger ones by a
 // group NTT of the parent vector (DIF: natural in, bit-reversed out), a pointwise scalar
 // multiplication by the NTT of each sibling polynomial, and two inverse group NTTs (DIT).  Group
-// NTT butterflies multiply points by (canonical) twiddles -- one variable-base scalar multiplication
-// per butterfly -- so the build costs ~ 1.5 N log^2 N scalar multiplications: a one-time setup per
-// (SRS, N), like the tau-derived basis (tests/test_gpu_tfree.py pins it to that basis; measured
-// cost and its extrapolation to 2^24: DESIGN.md).  The scalar side (the subproduct tree's
+// NTT butterflies multiply points by twiddles -- one variable-base scalar multiplication per
+// butterfly, split by the GLV endomorphism into two 127-bit halves walked jointly (xyzz_mul_glv),
+// in the lazy domain -- so the build costs ~ 1.5 N log^2 N scalar multiplications: a one-time setup
+// per (SRS, N), like the tau-derived basis (tests/test_gpu_tfree.py pins it to that basis; measured
+// cost: DESIGN.md 2.8).  The scalar side (the subproduct tree's
 // polynomials, stored monic with the leading 1 implicit) is negligible beside it.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -39,10 +42,32 @@ constexpr size_t TF_DIRECT_H = 4;  // children of <= 4 nodes: direct correlation
 // the kernels that multiply points by scalars: 3 waves per SIMD (168 VGPRs; the default bound let
 // the compiler take 258 registers, one wave per SIMD)
 #define TF_WAVES 3
+// the group NTT's butterflies (GLV joint multiplication: P, phi(P), their sum and the accumulator)
+#ifndef TF_NTT_WAVES
+#define TF_NTT_WAVES 2
+#endif
 
 __device__ __forceinline__ G1Xyzz xyzz_negate(const G1Xyzz &p) {
   G1Xyzz r = p;
   r.y = neg(p.y);
+  return r;
+}
+
+// dbl-2008-s-1 in the lazy domain (coordinates in [0, 2M), as xyzz_add_lazy): no final
+// subtractions in the products, Y3 as one reduction of M (S - X3) + Y (2M - W)
+__device__ __forceinline__ G1Xyzz xyzz_dbl_lazy(const G1Xyzz &p) {
+  if (fq_zero_lazy(p.zz) || fq_zero_lazy(p.y)) return G1Xyzz::inf();
+  const Fq U = add2_dev(p.y, p.y);
+  const Fq V = sqr_lazy_dev(U);
+  const Fq W = mul_lazy_dev(U, V);
+  const Fq S = mul_lazy_dev(p.x, V);
+  const Fq X2 = sqr_lazy_dev(p.x);
+  const Fq M = add2_dev(add2_dev(X2, X2), X2);
+  G1Xyzz r;
+  r.x = sub2_dev(sqr_lazy_dev(M), add2_dev(S, S));
+  r.y = mul2_lazy_dev(M, sub2_dev(S, r.x), p.y, const_minus_dev<FqCfg, true>(W));
+  r.zz = mul_lazy_dev(V, p.zz);
+  r.zzz = mul_lazy_dev(W, p.zzz);
   return r;
 }
 
@@ -59,14 +84,174 @@ __device__ G1Xyzz xyzz_mul_canon(const G1Xyzz &P, const Fr &k) {
     if (!started && w == 0) continue;
 #pragma unroll 1
     for (int b = 31; b >= 0; b--) {
-      if (started) acc = xyzz_dbl(acc);
+      if (started) acc = xyzz_dbl_lazy(acc);
       if ((w >> b) & 1u) {
-        acc = started ? xyzz_add(acc, P) : P;
+        acc = started ? xyzz_add_lazy(acc, P) : P;
         started = true;
       }
     }
   }
-  return acc;
+  return xyzz_canon(acc);
+}
+
+// ---- GLV: phi(x, y) = (beta x, y) equals lambda (x, y) on G1 (beta a primitive cube root of unity
+// in Fq, lambda the matching one in Fr: phi(G) = lambda G, checked against the C oracle when the
+// constants were derived), so k P = k1 P + k2 phi(P) with k = k1 + k2 lambda (mod r) and
+// |k1|, |k2| < 2^127: half the doublings of a 254-bit double-and-add.  The group NTT's twiddles are
+// split once per basis build on the host (Babai rounding in the reduced lattice basis
+// (a1, b1), (a2, b2) of {(a, b): a + b lambda = 0 mod r}; g1 = floor(b2 2^256 / r),
+// g2 = floor(-b1 2^256 / r)).
+struct GlvScalar {
+  uint32_t k1[4], k2[4];  // magnitudes
+  uint32_t neg;           // bit 0: k1 < 0, bit 1: k2 < 0
+};
+// beta in Montgomery form (canonical 0x30644e72e131a0295e6dd9e7e0acccb0c28f069fbb966e3de4bd44e5607cfd48)
+__constant__ uint32_t kGlvBeta[8] = {0x13e80b9cu, 0x3350c88eu, 0xdb5e56b9u, 0x7dce557cu,
+                                     0xb615564au, 0x6001b4b8u, 0x020217e0u, 0x2682e617u};
+
+// k1 P + k2 phi(P), joint left-to-right double-and-add (Straus-Shamir: P, phi(P) and their sum)
+// from bit 126; uniform per wave where the lanes share the scalar (the twiddles)
+__device__ G1Xyzz xyzz_mul_glv(const G1Xyzz &P, const GlvScalar &s) {
+  const G1Xyzz P1 = (s.neg & 1u) ? xyzz_negate(P) : P;
+  Fq beta;
+#pragma unroll
+  for (int q = 0; q < 8; q++) beta.v[q] = kGlvBeta[q];
+  G1Xyzz P2 = P;
+  P2.x = mul(P.x, beta);
+  if (s.neg & 2u) P2.y = neg(P.y);
+  const G1Xyzz P12 = xyzz_add(P1, P2);  // Straus-Shamir: one addition where both bits are set
+  G1Xyzz acc = G1Xyzz::inf();
+  bool started = false;
+#pragma unroll 1
+  for (int l = 3; l >= 0; l--) {
+    uint32_t w1 = 0, w2 = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // (a dynamic index would use scratch)
+      w1 = q == l ? s.k1[q] : w1;
+      w2 = q == l ? s.k2[q] : w2;
+    }
+    if (!started && (w1 | w2) == 0) continue;
+#pragma unroll 1
+    for (int b = 31; b >= 0; b--) {
+      if (started) acc = xyzz_dbl_lazy(acc);
+      const uint32_t d = ((w1 >> b) & 1u) | (((w2 >> b) & 1u) << 1);
+      if (d) {
+        const G1Xyzz &T = d == 3 ? P12 : d == 1 ? P1 : P2;
+        acc = started ? xyzz_add_lazy(acc, T) : T;
+        started = true;
+      }
+    }
+  }
+  return xyzz_canon(acc);  // the butterflies' canonical additions read it
+}
+
+// host: the lattice constants (64-bit limbs, little endian)
+static const uint64_t kGlvA1[2] = {0x8211bbeb7d4f1128ull, 0x6f4d8248eeb859fcull};
+static const uint64_t kGlvA2[1] = {0x89d3256894d213e3ull};
+static const uint64_t kGlvB1Abs[1] = {0x89d3256894d213e3ull};
+static const uint64_t kGlvB2[2] = {0x0be4e1541221250bull, 0x6f4d8248eeb859fdull};
+static const uint64_t kGlvG1[3] = {0x5398fd0300ff6565ull, 0x4ccef014a773d2d2ull, 0x2ull};
+static const uint64_t kGlvG2[2] = {0xd91d232ec7e0b3d7ull, 0x2ull};
+
+static void limbs_mul(const uint64_t *a, int na, const uint64_t *b, int nb, uint64_t *r) {  // r: na + nb limbs
+  for (int i = 0; i < na + nb; i++) r[i] = 0;
+  for (int i = 0; i < na; i++) {
+    unsigned __int128 c = 0;
+    for (int j = 0; j < nb; j++) {
+      c += (unsigned __int128)a[i] * b[j] + r[i + j];
+      r[i + j] = (uint64_t)c;
+      c >>= 64;
+    }
+    r[i + nb] = (uint64_t)c;
+  }
+}
+
+// |a - b| into r (n limbs); returns a < b
+static bool limbs_absdiff(const uint64_t *a, const uint64_t *b, uint64_t *r, int n) {
+  int c = 0;
+  for (int i = n - 1; i >= 0 && !c; i--) c = a[i] < b[i] ? -1 : a[i] > b[i] ? 1 : 0;
+  const uint64_t *x = c < 0 ? b : a, *y = c < 0 ? a : b;
+  unsigned __int128 br = 0;
+  for (int i = 0; i < n; i++) {
+    const unsigned __int128 d = (unsigned __int128)x[i] - y[i] - br;
+    r[i] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  return c < 0;
+}
+
+// canonical k < r -> (k1, k2); throws if a part exceeds 128 bits (it cannot: |k1|, |k2| < 2^127)
+static GlvScalar glv_split(const uint64_t k[4]) {
+  uint64_t p1[7], p2[6];
+  limbs_mul(k, 4, kGlvG1, 3, p1);
+  limbs_mul(k, 4, kGlvG2, 2, p2);
+  const uint64_t c1[3] = {p1[4], p1[5], p1[6]}, c2[2] = {p2[4], p2[5]};
+  uint64_t t1[5], t2[3], t[5], kk[5] = {k[0], k[1], k[2], k[3], 0}, k1[5];
+  limbs_mul(c1, 3, kGlvA1, 2, t1);
+  limbs_mul(c2, 2, kGlvA2, 1, t2);
+  unsigned __int128 cy = 0;
+  for (int i = 0; i < 5; i++) {
+    cy += (unsigned __int128)t1[i] + (i < 3 ? t2[i] : 0);
+    t[i] = (uint64_t)cy;
+    cy >>= 64;
+  }
+  const bool n1 = limbs_absdiff(kk, t, k1, 5);
+  uint64_t u1[4], u2[4], k2[4];
+  limbs_mul(c1, 3, kGlvB1Abs, 1, u1);
+  limbs_mul(c2, 2, kGlvB2, 2, u2);
+  const bool n2 = limbs_absdiff(u1, u2, k2, 4);
+  if (k1[2] | k1[3] | k1[4] | k2[2] | k2[3]) throw Error(TNS_ERR_INVALID_PARAMETERS, "GLV split out of range");
+  GlvScalar g;
+  for (int i = 0; i < 2; i++) {
+    g.k1[2 * i] = (uint32_t)k1[i];
+    g.k1[2 * i + 1] = (uint32_t)(k1[i] >> 32);
+    g.k2[2 * i] = (uint32_t)k2[i];
+    g.k2[2 * i + 1] = (uint32_t)(k2[i] >> 32);
+  }
+  g.neg = (n1 ? 1u : 0u) | (n2 ? 2u : 0u);
+  return g;
+}
+
+__global__ void __launch_bounds__(256) k_tf_canon_twiddles(const Fr *__restrict__ TW, size_t n, Fr *__restrict__ out) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = from_mont(TW[i]);
+}
+
+// the twiddle table TW[0..N) split for the group NTT (download, split on host threads, upload)
+static void glv_twiddles(Ctx *c, const Fr *TW, size_t N, DevBuf &out) {
+  DevBuf canon;
+  Fr *d_canon = (Fr *)canon.ensure(sizeof(Fr) * N);
+  k_tf_canon_twiddles<<<grid_for(N, 256, 4096), 256, 0, c->stream>>>(TW, N, d_canon);
+  TNS_LAUNCH_CHECK();
+  std::vector<Fr> h(N);
+  TNS_HIP(hipMemcpyAsync(h.data(), d_canon, sizeof(Fr) * N, hipMemcpyDeviceToHost, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
+  std::vector<GlvScalar> g(N);
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(16, N / 4096));
+  std::vector<std::thread> ths;
+  std::atomic<bool> bad(false);
+  auto work = [&](size_t t) {
+    for (size_t i = t; i < N; i += nt) {
+      uint64_t k[4];
+      for (int q = 0; q < 4; q++) k[q] = (uint64_t)h[i].v[2 * q] | ((uint64_t)h[i].v[2 * q + 1] << 32);
+      try {
+        g[i] = glv_split(k);
+      } catch (...) {
+        bad = true;
+      }
+    }
+  };
+  try {
+    for (size_t t = 1; t < nt; t++) ths.emplace_back(work, t);
+  } catch (...) {  // threads that could not start: their share runs here
+    for (size_t t = ths.size() + 1; t < nt; t++) work(t);
+  }
+  work(0);
+  for (auto &th : ths) th.join();
+  if (bad) throw Error(TNS_ERR_INVALID_PARAMETERS, "GLV split out of range");
+  GlvScalar *d = (GlvScalar *)out.ensure(sizeof(GlvScalar) * N);
+  TNS_HIP(hipMemcpyAsync(d, g.data(), sizeof(GlvScalar) * N, hipMemcpyHostToDevice, c->stream));
+  TNS_HIP(hipStreamSynchronize(c->stream));
 }
 
 // ---- scalar side: the subproduct tree ell_S, monic, leading coefficient implicit.  Level e holds
@@ -113,24 +298,24 @@ __global__ void __launch_bounds__(256) k_tf_fdit(Fr *__restrict__ X, size_t N, s
     X[b] = sub(x, y);
   }
 }
-__global__ void __launch_bounds__(256, TF_WAVES) k_tf_gdif(G1Xyzz *__restrict__ X, size_t N, size_t hs,
-                                                 const Fr *__restrict__ TW) {
+__global__ void __launch_bounds__(256, TF_NTT_WAVES) k_tf_gdif(G1Xyzz *__restrict__ X, size_t N, size_t hs,
+                                                 const GlvScalar *__restrict__ TG) {
   const size_t nB = N / (2 * hs), half = N / 2;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < half; t += (size_t)gridDim.x * blockDim.x) {
     const size_t j = t / nB, a = (t - j * nB) * 2 * hs + j, b = a + hs;
     const G1Xyzz x = X[a], y = X[b];
     X[a] = xyzz_add(x, y);
     const G1Xyzz d = xyzz_add(x, xyzz_negate(y));
-    X[b] = j ? xyzz_mul_canon(d, from_mont(TW[hs + j])) : d;
+    X[b] = j ? xyzz_mul_glv(d, TG[hs + j]) : d;
   }
 }
-__global__ void __launch_bounds__(256, TF_WAVES) k_tf_gdit(G1Xyzz *__restrict__ X, size_t N, size_t hs,
-                                                 const Fr *__restrict__ TW) {
+__global__ void __launch_bounds__(256, TF_NTT_WAVES) k_tf_gdit(G1Xyzz *__restrict__ X, size_t N, size_t hs,
+                                                 const GlvScalar *__restrict__ TG) {
   const size_t nB = N / (2 * hs), half = N / 2;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < half; t += (size_t)gridDim.x * blockDim.x) {
     const size_t j = t / nB, a = (t - j * nB) * 2 * hs + j, b = a + hs;
     const G1Xyzz x = X[a];
-    const G1Xyzz y = j ? xyzz_negate(xyzz_mul_canon(X[b], from_mont(TW[2 * hs - j]))) : X[b];
+    const G1Xyzz y = j ? xyzz_negate(xyzz_mul_glv(X[b], TG[2 * hs - j])) : X[b];
     X[a] = xyzz_add(x, y);
     X[b] = xyzz_add(x, xyzz_negate(y));
   }
@@ -210,7 +395,7 @@ __global__ void __launch_bounds__(256) k_tf_scale_canon(Fr *__restrict__ S, size
     S[idx] = from_mont(mul(S[idx], s));
 }
 // Y[idx] = H^[idx] * SR[idx] (left child), H^[idx] *= SL[idx] (right child), in bit-reversed order
-__global__ void __launch_bounds__(256, TF_WAVES) k_tf_pointwise(G1Xyzz *__restrict__ Hh, const Fr *__restrict__ SL,
+__global__ void __launch_bounds__(256, TF_NTT_WAVES) k_tf_pointwise(G1Xyzz *__restrict__ Hh, const Fr *__restrict__ SL,
                                                       const Fr *__restrict__ SR, size_t N, G1Xyzz *__restrict__ Y) {
   for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < N; idx += (size_t)gridDim.x * blockDim.x) {
     const G1Xyzz p = Hh[idx];
@@ -228,12 +413,12 @@ __global__ void __launch_bounds__(256) k_tf_take(const G1Xyzz *__restrict__ Yl, 
   }
 }
 
-static void g_ntt(hipStream_t st, G1Xyzz *X, size_t N, size_t M, const Fr *TW, bool inverse) {
+static void g_ntt(hipStream_t st, G1Xyzz *X, size_t N, size_t M, const GlvScalar *TG, bool inverse) {
   const unsigned g = grid_for(N / 2, 256, 1u << 20);
   if (!inverse) {
-    for (size_t hs = M / 2; hs >= 1; hs /= 2) k_tf_gdif<<<g, 256, 0, st>>>(X, N, hs, TW);
+    for (size_t hs = M / 2; hs >= 1; hs /= 2) k_tf_gdif<<<g, 256, 0, st>>>(X, N, hs, TG);
   } else {
-    for (size_t hs = 1; hs < M; hs *= 2) k_tf_gdit<<<g, 256, 0, st>>>(X, N, hs, TW);
+    for (size_t hs = 1; hs < M; hs *= 2) k_tf_gdit<<<g, 256, 0, st>>>(X, N, hs, TG);
   }
   TNS_LAUNCH_CHECK();
 }
@@ -296,6 +481,9 @@ const LagrangeBasis *lagrange_basis_from_powers_dev(Ctx *c, const Srs &srs, size
         }
       }
       // group side, root to leaves: H holds every node's vector of the current level
+      DevBuf tgb;
+      glv_twiddles(c, TW, N, tgb);
+      const GlvScalar *TG = tgb.as<GlvScalar>();
       DevBuf hb, hh, yb;
       G1Xyzz *H = (G1Xyzz *)hb.ensure(sizeof(G1Xyzz) * N), *Hh = (G1Xyzz *)hh.ensure(sizeof(G1Xyzz) * N);
       k_tf_from_affine<<<gN, 256, 0, st>>>(g, N, H);
@@ -321,11 +509,11 @@ const LagrangeBasis *lagrange_basis_from_powers_dev(Ctx *c, const Srs &srs, size
         k_tf_scale_canon<<<gN, 256, 0, st>>>(B, N, iM);
         TNS_LAUNCH_CHECK();
         TNS_HIP(hipMemcpyAsync(Hh, H, sizeof(G1Xyzz) * N, hipMemcpyDeviceToDevice, st));
-        g_ntt(st, Hh, N, M, TW, false);
+        g_ntt(st, Hh, N, M, TG, false);
         k_tf_pointwise<<<gS, 256, 0, st>>>(Hh, A, B, N, Y);  // Y: left child (SR), Hh: right child (SL)
         TNS_LAUNCH_CHECK();
-        g_ntt(st, Y, N, M, TW, true);
-        g_ntt(st, Hh, N, M, TW, true);
+        g_ntt(st, Y, N, M, TG, true);
+        g_ntt(st, Hh, N, M, TG, true);
         k_tf_take<<<gN, 256, 0, st>>>(Y, Hh, N, h, H);
         TNS_LAUNCH_CHECK();
       }
