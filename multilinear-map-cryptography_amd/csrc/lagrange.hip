@@ -77,7 +77,13 @@ __global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, si
     __syncthreads();
     hi = mul(hi, o);
   }
-  if (tid == 0) inv_total = inv(hi);  // hi of thread 0 = the block's product
+  // hi of thread 0 = the block's product; its inverse is the kernel's latency: the binary extended
+  // Euclid (TNS_CHAIN_INV_FERMAT=1 build: the Fermat chain)
+#if defined(TNS_CHAIN_INV_FERMAT)
+  if (tid == 0) inv_total = inv(hi);
+#else
+  if (tid == 0) inv_total = inv_binary_dev(hi);
+#endif
   sh[tid] = lo;
   __syncthreads();
   const Fr before = tid ? sh[tid - 1] : Fr::one();  // prod over s < t

@@ -11,7 +11,7 @@ for rep in $(seq 1 $reps); do
   for v in default $tag; do
     if [ $v = default ]; then lib=$L/libtns.so; else lib=$L/libtns_$v.so; fi
     TNS_LIB=$lib timeout -k 10 200 python3 -u bench.py --no-extras --steps 10 --warmup 3 > $out/c4_${v}_$rep.jsonl 2> $out/c4_${v}_$rep.err || exit $?
-    TNS_LIB=$lib timeout -k 10 100 python3 tools/msm_trace.py 20 20 > $out/c2_${v}_$rep.txt 2>&1 || exit $?
+    TNS_LIB=$lib timeout -k 10 100 python3 tools/${EXTRA:-msm_trace.py 20 20} > $out/c2_${v}_$rep.txt 2>&1 || exit $?
     echo "$v rep $rep C4: $(python3 -c "import json; d=json.loads(open('$out/c4_${v}_$rep.jsonl').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['roofline']['avg_launch_ms'], d['stages_ms_per_step']['msm_accumulate'])")  C2: $(tail -n 1 $out/c2_${v}_$rep.txt)"
   done
 done
