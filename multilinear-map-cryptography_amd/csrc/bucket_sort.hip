@@ -696,6 +696,35 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t *__r
   }
 }
 
+// up to SCAN_SMALL counts in ONE launch: one block of 1024 threads walks the array in rounds of
+// 1024 x 16 (the segment-count scans of the later passes: 257 .. 65 537 entries, where three
+// launches of a few microseconds each were most of the cost)
+constexpr size_t SCAN_SMALL = (size_t)1 << 17;
+__global__ void __launch_bounds__(1024) k_scan_single(const uint32_t *__restrict__ in, size_t n,
+                                                      uint32_t *__restrict__ out) {
+  __shared__ uint32_t lds[1024 / 64];
+  uint32_t carry = 0;
+  for (size_t b0 = 0; b0 < n; b0 += (size_t)1024 * SCAN_ITEMS) {
+    const size_t base = b0 + (size_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t x[SCAN_ITEMS];
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) x[k] = base + k < n ? in[base + k] : 0u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+      const uint32_t v = x[k];
+      x[k] = s;
+      s += v;
+    }
+    uint32_t tot;
+    const uint32_t off = carry + block_excl_scan<1024>(s, lds, tot);
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+      if (base + k < n) out[base + k] = off + x[k];
+    carry += tot;
+  }
+}
+
 // out[i] = sum_{j < i} in[j] for i < n (in and out distinct device arrays; 16-byte vector
 // loads / stores where the array is 16-byte aligned)
 static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint32_t *out, size_t n) {
@@ -703,6 +732,11 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint
   const size_t tiles = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (tiles == 1) {
     k_scan_apply<<<1, SCAN_THREADS, 0, st>>>(in, n, nullptr, out);
+    TNS_LAUNCH_CHECK();
+    return;
+  }
+  if (n <= SCAN_SMALL) {
+    k_scan_single<<<1, 1024, 0, st>>>(in, n, out);
     TNS_LAUNCH_CHECK();
     return;
   }
