@@ -121,6 +121,22 @@ __device__ __forceinline__ void tile_scalars(const DigitArgs &A, size_t a, size_
   }
 }
 
+// The tile a scatter block works on.  Blocks are dealt round-robin over the 8 XCDs (blocks b and
+// b + 8 share one, MI355X_MICROARCH.md), and consecutive tiles write adjacent runs into every bin
+// (a run's last line is the next tile's first): TNS_BS_XCD builds map contiguous tile ranges to
+// one XCD (the guide's bijective remap) so those shared lines merge in one L2 before write-back.
+#ifndef TNS_BS_XCD
+#define TNS_BS_XCD 0
+#endif
+__device__ __forceinline__ size_t scatter_tile() {
+#if TNS_BS_XCD
+  const size_t nwg = gridDim.x, orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+#else
+  return blockIdx.x;
+#endif
+}
+
 // out[d] = sum_{d' < d} h[d'] for d < nb <= 2 * BS_BLOCK (two bins per thread)
 __device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out, int nb, uint32_t *wsum) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -221,7 +237,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1(DigitArgs A, int shift
                                                           uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   __shared__ uint32_t lk[TILE], lv[TILE];
-  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  const size_t tile = scatter_tile(), a = tile * A.spb, b = min(A.n, a + A.spb);
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
     h[d] = 0;
     goff[d] = offs[(size_t)d * T1 + tile];
@@ -304,7 +320,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
                                                              uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   __shared__ uint32_t lk[TILE], lv[TILE];
-  const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  const size_t tile = scatter_tile(), a = tile * A.spb, b = min(A.n, a + A.spb);
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
     h[d] = 0;
     goff[d] = offs[(size_t)d * T1 + tile];
@@ -506,7 +522,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
   __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
   constexpr int IPT = TILE / BS_BLOCK;
   __shared__ uint32_t lk[TILE], lv[PK == 2 ? 1 : TILE];
-  const size_t g = blockIdx.x;
+  const size_t g = scatter_tile();
   if (g >= (G.ident ? S : G.tbase[S])) return;
   uint32_t s, tb, Ts;
   tile_geom(G, g, s, tb, Ts);
