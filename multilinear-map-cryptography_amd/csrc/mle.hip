@@ -29,8 +29,31 @@ struct ScTables {
 struct ScTerms {
   Fr coeff[MAX_SC_TERMS];
   int8_t tab[MAX_SC_TERMS][3];
+  // coefficient kinds (set by sc_terms): 0 one, 1 minus one, 2 two, 3 any -- the round kernel
+  // multiplies by a coefficient only for kind 3 (the Twist-shaped A V - O O V + 2 O: 3 products
+  // per point instead of 6)
+  int8_t kind[MAX_SC_TERMS];
   int n;
 };
+
+// the host side of ScTerms: tables checked against k, coefficient kinds classified
+static ScTerms sc_terms(const SumcheckTerm *terms, int n_terms, int k) {
+  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
+  ScTerms st{};
+  st.n = n_terms;
+  const Fr one = Fr::one(), two = add(one, one), minus_one = neg(one);
+  for (int t = 0; t < n_terms; t++) {
+    const Fr &c = terms[t].coeff;
+    st.coeff[t] = c;
+    st.kind[t] = c == one ? 0 : c == minus_one ? 1 : c == two ? 2 : 3;
+    for (int j = 0; j < 3; j++) {
+      const int ix = terms[t].tab[j];
+      if (ix >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
+      st.tab[t][j] = (int8_t)ix;
+    }
+  }
+  return st;
+}
 
 // ---------------------------------------------------------------- wave/block reductions
 __device__ __forceinline__ Fr shfl_down_fr(const Fr &a, int d) {
@@ -142,6 +165,7 @@ __global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms ter
 #pragma unroll
       for (int i = 0; i < MAX_SC_TABLES; i++)
         if (i < k) d[i] = sub(f1[i], f0[i]);
+#pragma unroll  // (a runtime x put acc[] in scratch memory)
       for (int x = 0; x < 4; x++) {
         if (SKIP1 && x == 1) continue;
         Fr vx[MAX_SC_TABLES];
@@ -156,7 +180,8 @@ __global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms ter
         }
         Fr sum = Fr::zero();
         for (int tt = 0; tt < terms.n; tt++) {
-          Fr p = terms.coeff[tt];
+          Fr p = Fr::one();
+          bool first = true;
 #pragma unroll
           for (int j = 0; j < 3; j++) {
             int ix = terms.tab[tt][j];
@@ -165,9 +190,14 @@ __global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms ter
 #pragma unroll
               for (int q = 1; q < MAX_SC_TABLES; q++)
                 if (ix == q) v = vx[q];
-              p = mul(p, v);
+              p = first ? v : mul(p, v);
+              first = false;
             }
           }
+          const int kind = terms.kind[tt];  // (uniform: the coefficient only where it is not +-1 or 2)
+          if (kind == 1) p = neg(p);
+          else if (kind == 2) p = add(p, p);
+          else if (kind == 3) p = mul(terms.coeff[tt], p);
           sum = add(sum, p);
         }
         acc[x] = add(acc[x], sum);
@@ -370,16 +400,7 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
 // X = 0 and X = 1 of the fused round kernel, added
 Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const SumcheckTerm *terms, int n_terms) {
   if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "1 to 4 sum-check tables");
-  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
-  ScTerms st{};
-  st.n = n_terms;
-  for (int t = 0; t < n_terms; t++) {
-    st.coeff[t] = terms[t].coeff;
-    for (int j = 0; j < 3; j++) {
-      if (terms[t].tab[j] >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
-      st.tab[t][j] = (int8_t)terms[t].tab[j];
-    }
-  }
+  const ScTerms st = sc_terms(terms, n_terms, k);
   if (nv == 0) {
     Fr v[MAX_SC_TABLES];
     for (int i = 0; i < k; i++) TNS_HIP(hipMemcpyAsync(&v[i], tables[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
@@ -408,17 +429,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_vals, Fr *final_eval) {
   if (k < 0 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
-  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
-  ScTerms st{};
-  st.n = n_terms;
-  for (int t = 0; t < n_terms; t++) {
-    st.coeff[t] = terms[t].coeff;
-    for (int j = 0; j < 3; j++) {
-      int ix = terms[t].tab[j];
-      if (ix >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
-      st.tab[t][j] = (int8_t)ix;
-    }
-  }
+  const ScTerms st = sc_terms(terms, n_terms, k);
   const bool has_terms = n_terms > 0;
   const size_t n = (size_t)1 << nv;
   // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)); round 1
