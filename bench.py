@@ -342,7 +342,7 @@ def sumcheck_generic(ts, ctx, logs):
                          "alg_bytes": ex["bytes"] / reps,
                          "achieved_GBps": round(gbs, 1) if gbs else None,
                          "hbm_frac": round(gbs / HBM_PEAK_GBPS, 4) if gbs else None,
-                         "bound": "Fr multiply (6 products per composition point x 4 points + 2 per fold)"}
+                         "bound": "Fr multiply (3 products per composition point x 3 points -- g(1) comes from the claim -- + 2 per table per fold)"}
         del tabs
     return out
 
