@@ -4,6 +4,7 @@ matches the oracle.  No device compute is called here."""
 import ctypes as C
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -42,6 +43,18 @@ def test_version_and_no_silent_fallback():
         assert st == 101, N.last_error()
         with pytest.raises(ts.TwistAndShoutError):
             ts.Context(0)
+
+
+def test_c_host_refuses_without_device():
+    """The plain C host of the ABI (examples/twist_prove.c, built by build()) links against
+    libtns.so alone and, with no device, exits 3 with the library's error -- no CPU fallback."""
+    exe = os.path.join(ROOT, "multilinear-map-cryptography_amd", "examples", "twist_prove")
+    assert os.path.exists(exe), "build() builds examples/twist_prove"
+    if N.load().tns_device_count() != 0:
+        pytest.skip("a device is visible: tests/test_gpu_c_host.py runs it")
+    r = subprocess.run([exe, "3", "8"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 3, (r.returncode, r.stderr)
+    assert "no HIP device" in r.stderr
 
 
 def test_host_transcript_matches_oracle():
