@@ -46,15 +46,16 @@ def test_version_and_no_silent_fallback():
 
 
 def test_c_host_refuses_without_device():
-    """The plain C host of the ABI (examples/twist_prove.c, built by build()) links against
+    """The plain C host of the ABI (examples/prove.c, built by build()) links against
     libtns.so alone and, with no device, exits 3 with the library's error -- no CPU fallback."""
-    exe = os.path.join(ROOT, "multilinear-map-cryptography_amd", "examples", "twist_prove")
-    assert os.path.exists(exe), "build() builds examples/twist_prove"
+    exe = os.path.join(ROOT, "multilinear-map-cryptography_amd", "examples", "prove")
+    assert os.path.exists(exe), "build() builds examples/prove"
     if N.load().tns_device_count() != 0:
         pytest.skip("a device is visible: tests/test_gpu_c_host.py runs it")
-    r = subprocess.run([exe, "3", "8"], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 3, (r.returncode, r.stderr)
-    assert "no HIP device" in r.stderr
+    for proto in ("twist", "shout"):
+        r = subprocess.run([exe, proto, "3", "8"], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 3, (r.returncode, r.stderr)
+        assert "no HIP device" in r.stderr
 
 
 def test_host_transcript_matches_oracle():
