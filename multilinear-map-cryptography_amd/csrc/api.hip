@@ -236,8 +236,11 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
   allgather_sum_g1_pair(c, m, part, out);
 }
 
+// after_quotients (optional): called once the quotient kernel is queued (the side-stream folds'
+// placement A/B, TNS_FOLDS_AT=1)
 static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, const Fr &z, Fr value[2],
-                            G1Affine proof[2], DevBuf &sbuf0, DevBuf &sbuf1, Comm &m) {
+                            G1Affine proof[2], DevBuf &sbuf0, DevBuf &sbuf1, Comm &m,
+                            const std::function<void()> &after_quotients = nullptr) {
   if (!p0.basis || !p1.basis || fr_is_node(z, p0.N) || fr_is_node(z, p1.N)) {
     open_evals(c, srs, p0, z, &value[0], &proof[0], sbuf0, m);
     open_evals(c, srs, p1, z, &value[1], &proof[1], sbuf0, m);
@@ -272,6 +275,7 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
     lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
     lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
   }
+  if (after_quotients) after_quotients();
   G1Xyzz pp[2];
   msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits},
                MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr}, pp);
@@ -883,16 +887,26 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   // ... and the folds binding this rank's tables at r_0 .. r_{nv_loc-1} (the MLE values the
   // closure evaluates, src/sumcheck.rs:104) run on the side stream under the openings; their
   // values are collected at the end of the proof
-  {
+  Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
+  bool folds_queued = false;
+  auto queue_folds = [&]() {
+    if (folds_queued) return;
+    folds_queued = true;
     hipEvent_t ready;
     TNS_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
     TNS_HIP(hipEventRecord(ready, c->stream));  // the tables were written on the context stream
     TNS_HIP(hipStreamWaitEvent(c->side, ready, 0));
     (void)hipEventDestroy(ready);
-  }
-  Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
-  sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals, flags, n_flags);
-  TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
+    sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals, flags, n_flags);
+    TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
+  };
+  // TNS_FOLDS_AT=1 (A/B): queue the folds behind the quotient kernel, i.e. under the opening
+  // sorts instead of beside the barycentric pass
+  static const int folds_at = [] {
+    const char *e = getenv("TNS_FOLDS_AT");
+    return e ? atoi(e) : 0;
+  }();
+  if (folds_at != 1 || nv < 1) queue_folds();
   const Fr fe = Fr::zero();
   out->num_rounds = nv;
   std::memcpy(out->round_polynomials, rounds.data(), 128 * (size_t)nv);
@@ -909,7 +923,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     std::memcpy(out->opening_point, &z, 32);
     Fr v[2];
     G1Affine pi[2];
-    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m);
+    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m, queue_folds);
     store_proj(pi[0], out->opening_proofs[0]);
     store_proj(pi[1], out->opening_proofs[1]);
     std::memcpy(out->final_evaluations[0], &v[0], 32);
@@ -917,6 +931,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     out->num_openings = 2;
   }
   timing[4] = t_open.ms();
+  queue_folds();  // (a no-op unless the openings took a path without the hook)
   // the side stream's bound table values; with several ranks each holds its slice's values at
   // r_0 .. r_{nv_loc-1}, and the last lr challenges fold the allgathered rank values
   TNS_HIP(hipStreamSynchronize(c->side));
