@@ -249,9 +249,17 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
   Fr *q0 = (Fr *)sbuf0.ensure(sizeof(Fr) * p0.cnt), *q1 = (Fr *)sbuf1.ensure(sizeof(Fr) * p1.cnt);
   Fr part[4];
   const bool same_nodes = p0.N == p1.N && p0.first == p1.first && p0.cnt == p1.cnt;
+  // the shared-inverse pass hands the MSMs canonical quotients and their bit lengths; its
+  // inverses come out canonical too, so the quotient kernel needs no reduction pass
+  // (TNS_CANON_INV=0: Montgomery inverses and a from_mont per quotient, A/B)
+  static const bool canon_env = [] {
+    const char *e = getenv("TNS_CANON_INV");
+    return !(e && e[0] == '0');
+  }();
+  const bool canon_q = same_nodes && p0.cnt > 64, canon_inv = canon_q && canon_env;
   if (same_nodes) {  // Twist: one batch inversion for both vectors (inverses land in q1)
     Fr p3[3];
-    lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3);
+    lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3, canon_inv);
     part[0] = part[2] = p3[0];
     part[1] = p3[1];
     part[3] = p3[2];
@@ -267,10 +275,9 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
       S[k] = add(S[k], all[4 * (size_t)r + 2 * k + 1]);
     }
   for (int k = 0; k < 2; k++) value[k] = mul(ell[k], S[k]);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
-  // the shared-inverse pass hands the MSMs canonical quotients and their bit lengths
-  unsigned *qbits = same_nodes && p0.cnt > 64 ? (unsigned *)c->qbits.ensure(2 * sizeof(unsigned)) : nullptr;
+  unsigned *qbits = canon_q ? (unsigned *)c->qbits.ensure(2 * sizeof(unsigned)) : nullptr;
   if (same_nodes) {
-    lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1, qbits);
+    lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1, qbits, canon_inv);
   } else {
     lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
     lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);

@@ -565,11 +565,13 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
                                Fr *ell_part, Fr *sum_part);
 // q_i = (v - y_i) * inv_i in place: the quotient's values on the slice
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
+// canon_inv: inv receives the inverses in canonical form (for the CI quotient kernel)
 void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
-                                Fr *inv, Fr parts[3]);
-// bits != nullptr: q0 / q1 come out CANONICAL with their largest bit lengths in bits[0..1]
+                                Fr *inv, Fr parts[3], bool canon_inv = false);
+// bits != nullptr: q0 / q1 come out CANONICAL with their largest bit lengths in bits[0..1];
+// canon_inv (requires bits): inv holds canonical inverses (lagrange_open_partial2_dev's canon_inv)
 void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
-                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits);
+                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits, bool canon_inv = false);
 // quotient values for an opening AT the node j0 (value y_j0), unsharded
 void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q);
 bool fr_is_node(const Fr &x, size_t N);

@@ -53,8 +53,10 @@ __global__ void __launch_bounds__(256) k_node_chain(Fr x, size_t n, size_t T, Fr
 // icp[t] = 1 / cp[t] for t < T by one batch inversion per block of 256 chains (prefix and suffix
 // products in LDS, one Fermat inverse per block instead of one per chain: those were about a
 // third of k_node_finish2's multiplies).  A zero chain product gets 0 and leaves its block's
-// other inverses intact.  blockDim.x == 256.
-__global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, size_t T, Fr *__restrict__ icp) {
+// other inverses intact.  scale multiplies every inverse (the raw 1 = R^-1: canonical outputs,
+// see lagrange_open_partial2_dev).  blockDim.x == 256.
+__global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, size_t T, Fr *__restrict__ icp,
+                                                   Fr scale) {
   __shared__ Fr sh[256];
   __shared__ Fr inv_total;
   const int tid = threadIdx.x;
@@ -80,9 +82,9 @@ __global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, si
   // hi of thread 0 = the block's product; its inverse is the kernel's latency: the binary extended
   // Euclid (TNS_CHAIN_INV_FERMAT=1 build: the Fermat chain)
 #if defined(TNS_CHAIN_INV_FERMAT)
-  if (tid == 0) inv_total = inv(hi);
+  if (tid == 0) inv_total = mul(inv(hi), scale);
 #else
-  if (tid == 0) inv_total = inv_binary_dev(hi);
+  if (tid == 0) inv_total = mul(inv_binary_dev(hi), scale);
 #endif
   sh[tid] = lo;
   __syncthreads();
@@ -162,10 +164,11 @@ __global__ void __launch_bounds__(256) k_node_finish(Fr x, size_t n, size_t T, F
 
 // k_node_finish<false> for two vectors on the same nodes: the inverses are shared.
 //   inv[i] = inv_i;  sp[t] = sum_chain w_i y0_i inv_i,  sp[T + t] = sum_chain w_i y1_i inv_i
+// scale: as k_chain_inv's (applied here when the chain products come uninverted)
 __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, Fr Tm, const Fr *pre,
-                                                      const Fr *__restrict__ cp, bool inverted, const Fr *__restrict__ w,
-                                                      const Fr *__restrict__ y0, const Fr *__restrict__ y1,
-                                                      Fr *invs, Fr *__restrict__ sp) {
+                                                      const Fr *__restrict__ cp, bool inverted, Fr scale,
+                                                      const Fr *__restrict__ w, const Fr *__restrict__ y0,
+                                                      const Fr *__restrict__ y1, Fr *invs, Fr *__restrict__ sp) {
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
   if (t >= T) return;
   if (t >= n) {
@@ -175,7 +178,7 @@ __global__ void __launch_bounds__(256) k_node_finish2(Fr x, size_t n, size_t T, 
   const size_t cnt = (n - 1 - t) / T;
   size_t i = t + cnt * T;
   Fr d = sub(x, from_u64<FrCfg>((uint64_t)i));
-  Fr iv = inverted ? cp[t] : inv(cp[t]);  // cp: the chain inverses (k_chain_inv) or products
+  Fr iv = inverted ? cp[t] : mul(inv(cp[t]), scale);  // cp: the chain inverses (k_chain_inv) or products
   Fr s0 = Fr::zero(), s1 = Fr::zero();
   for (;;) {
     const Fr inv_i = mul(iv, pre[i]);
@@ -205,13 +208,20 @@ __global__ void __launch_bounds__(256) k_node_quotient2(const Fr *__restrict__ y
 // k_node_quotient2 producing what the two opening MSMs consume: the CANONICAL quotient values
 // (the bucket sort reads digits of canonical scalars) and each vector's largest bit length
 // (the MSM's window plan) -- msm.hip's k_scalar_bits pass over q0 / q1 is folded in here.
+// CI: the inverses are stored canonical (raw integers, i.e. the Montgomery forms of inv / R), so
+// the Montgomery product (v - y) * inv already IS the canonical quotient -- no reduction pass.
+template <bool CI>
 __global__ void __launch_bounds__(256) k_node_quotient2_canon(const Fr *__restrict__ y0, const Fr *__restrict__ y1,
                                                               Fr v0, Fr v1, size_t n, const Fr *invs,
                                                               Fr *__restrict__ q0, Fr *q1, unsigned *__restrict__ bits) {
   unsigned b0 = 0, b1 = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const Fr iv = invs[i];
-    const Fr c0 = from_mont(mul(sub(v0, y0[i]), iv)), c1 = from_mont(mul(sub(v1, y1[i]), iv));
+    Fr c0 = mul(sub(v0, y0[i]), iv), c1 = mul(sub(v1, y1[i]), iv);
+    if (!CI) {
+      c0 = from_mont(c0);
+      c1 = from_mont(c1);
+    }
     q0[i] = c0;
     q1[i] = c1;
     b0 = max(b0, fr_bit_length(c0));
@@ -308,7 +318,8 @@ struct NodeSweep {
 };
 
 // chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
-static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_t skip = SIZE_MAX) {
+static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_t skip = SIZE_MAX,
+                                   const Fr &scale = Fr::one()) {
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
@@ -324,7 +335,7 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   s.icp = s.cp;
   if (s.inverted) {
     s.icp = s.dev + 4 + 256;
-    k_chain_inv<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(s.cp, s.T, s.icp);
+    k_chain_inv<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(s.cp, s.T, s.icp, scale);
     TNS_LAUNCH_CHECK();
   }
   return s;
@@ -419,15 +430,22 @@ void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q)
 
 // Two vectors on the same nodes, opened at the same z (Twist: addresses and values): one
 // batch inversion serves both.  parts = {ell, sum0, sum1}; inv receives the shared inverses.
+// canon_inv: the inverses are written canonical (every chain inverse scaled by R^-1, the raw 1;
+// the products along the chain keep the factor), for lagrange_quotient_finish2_dev's CI form;
+// the sums then carry it too and are scaled back by R (the raw R^2) after the readback.
 void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
-                                Fr *inv, Fr parts[3]) {
+                                Fr *inv, Fr parts[3], bool canon_inv) {
   TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);  // pre write/read, inv write, y0, y1, w
   const Fr *w = bary_weights(c, N, first, cnt);
   const Fr xs = fr_shift(z, first);
-  NodeSweep s = node_sweep_begin(c, xs, cnt, inv);
-  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.icp, s.inverted, w, y0,
-                                                                      y1, inv,
-                                                                      s.sp);
+  Fr scale = Fr::one();
+  if (canon_inv) {
+    scale = Fr::zero();
+    scale.v[0] = 1;
+  }
+  NodeSweep s = node_sweep_begin(c, xs, cnt, inv, SIZE_MAX, scale);
+  k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.icp, s.inverted, scale,
+                                                                      w, y0, y1, inv, s.sp);
   TNS_LAUNCH_CHECK();
   k_sum_reduce<<<1, 1024, 0, c->stream>>>(s.sp, s.T, s.dev + 1);
   TNS_LAUNCH_CHECK();
@@ -435,14 +453,22 @@ void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, si
   TNS_LAUNCH_CHECK();
   TNS_HIP(hipMemcpyAsync(parts, s.dev, 3 * sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
   TNS_HIP(hipStreamSynchronize(c->stream));
+  if (canon_inv) {
+    Fr r2;
+    for (int i = 0; i < 8; i++) r2.v[i] = FrCfg::R2[i];
+    parts[1] = mul(parts[1], r2);
+    parts[2] = mul(parts[2], r2);
+  }
 }
 
 void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,
-                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits) {
+                                   const Fr *inv, Fr *q0, Fr *q1, unsigned *bits, bool canon_inv) {
   TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);
+  if (canon_inv && !bits) throw Error(TNS_ERR_INVALID_PARAMETERS, "canonical inverses give canonical quotients only");
   if (bits) {
     TNS_HIP(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned), c->stream));
-    k_node_quotient2_canon<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1, bits);
+    auto kern = canon_inv ? k_node_quotient2_canon<true> : k_node_quotient2_canon<false>;
+    kern<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1, bits);
   } else {
     k_node_quotient2<<<grid_for(cnt, 256), 256, 0, c->stream>>>(y0, y1, v0, v1, cnt, inv, q0, q1);
   }
