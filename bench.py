@@ -88,6 +88,9 @@ def parse():
     ap.add_argument("--comm", choices=["torch", "rccl"], default="torch",
                     help="sharded proof exchange: torch.distributed process group (nccl = RCCL) or the "
                          "library's own RCCL communicator")
+    ap.add_argument("--exchange-timeout", type=float, default=300.0,
+                    help="N > 1: deadline in seconds of one exchange step of the sharded proof; a step that "
+                         "misses it ends the run with exit status 3 and names the rank and step")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="testing aid: every rank on device 0 with a gloo process group (one-GPU box)")
     ap.add_argument("--no-msm-tables", action="store_true",
@@ -159,6 +162,110 @@ def max_over_ranks(pg, local, x):
 
 
 ROOF_KERNEL = "msm_accumulate"  # the dominant stage by device time (every stage timed: stages_ms_per_step)
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _dpm_current(text):
+    """Current level of a pp_dpm_* table ('1: 2100Mhz *') as MHz."""
+    if not text:
+        return None
+    for line in text.splitlines():
+        if line.rstrip().endswith("*"):
+            tok = line.split(":", 1)[-1].strip().rstrip("*").strip().lower().replace("mhz", "")
+            try:
+                return float(tok)
+            except ValueError:
+                return None
+    return None
+
+
+class DeviceState:
+    """The card's clocks, power and temperature around the timed region (the driver's numbers
+    differ box to box by several per cent; this is what tells a slow box from a slow build).
+    Sources: hipDeviceProp_t (tns_device_info_get: rated clocks, PCI bus id) and the amdgpu sysfs
+    files of that PCI device (pp_dpm_sclk / pp_dpm_mclk current levels, hwmon power cap, power,
+    temperatures, the board serial as the box identifier); a sampler thread reads the current
+    sclk / power / edge temperature every 100 ms while the steps run.  Missing files are null."""
+
+    def __init__(self, ts, device):
+        self.info = None
+        try:
+            self.info = ts.device_info(device)
+        except Exception as e:  # the record is diagnostic; never fail the bench over it
+            self.info = {"error": str(e)}
+        bus = (self.info or {}).get("pci_bus_id")
+        self.dev = f"/sys/bus/pci/devices/{bus}" if bus else None
+        self.hwmon = None
+        if self.dev and os.path.isdir(os.path.join(self.dev, "hwmon")):
+            hw = sorted(os.listdir(os.path.join(self.dev, "hwmon")))
+            if hw:
+                self.hwmon = os.path.join(self.dev, "hwmon", hw[0])
+        self.samples = []
+        self._stop = None
+        self._thread = None
+
+    def _hw(self, name, scale):
+        if not self.hwmon:
+            return None
+        v = _read(os.path.join(self.hwmon, name))
+        try:
+            return round(int(v) / scale, 2) if v is not None else None
+        except ValueError:
+            return None
+
+    def snapshot(self):
+        d = self.dev
+        return {"t": round(time.time(), 3),
+                "sclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_sclk"))) if d else None,
+                "mclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_mclk"))) if d else None,
+                "fclk_mhz": _dpm_current(_read(os.path.join(d, "pp_dpm_fclk"))) if d else None,
+                "power_w": self._hw("power1_average", 1e6) or self._hw("power1_input", 1e6),
+                "power_cap_w": self._hw("power1_cap", 1e6),
+                "temp_edge_c": self._hw("temp1_input", 1e3),
+                "temp_hotspot_c": self._hw("temp2_input", 1e3),
+                "temp_mem_c": self._hw("temp3_input", 1e3),
+                "perf_level": _read(os.path.join(d, "power_dpm_force_performance_level")) if d else None}
+
+    def start(self):
+        import threading
+
+        self.begin = self.snapshot()
+        self._stop = threading.Event()
+
+        def run():
+            while not self._stop.wait(0.1):
+                s = self.snapshot()
+                self.samples.append((s["sclk_mhz"], s["power_w"], s["temp_edge_c"]))
+
+        self._thread = threading.Thread(target=run, daemon=True)
+        self._thread.start()
+
+    def stop(self):
+        if self._thread is not None:
+            self._stop.set()
+            self._thread.join()
+        self.end = self.snapshot()
+
+    def record(self):
+        def stat(i):
+            xs = [s[i] for s in self.samples if s[i] is not None]
+            if not xs:
+                return None
+            return {"min": min(xs), "mean": round(sum(xs) / len(xs), 1), "max": max(xs), "n": len(xs)}
+
+        return {"device": self.info, "sysfs": self.dev if self.dev and os.path.isdir(self.dev) else None,
+                "host": platform.node(), "board_serial": _read(os.path.join(self.dev, "serial_number")) if self.dev
+                else None, "unique_id": _read(os.path.join(self.dev, "unique_id")) if self.dev else None,
+                "start": getattr(self, "begin", None), "end": getattr(self, "end", None),
+                "during": {"sclk_mhz": stat(0), "power_w": stat(1), "temp_edge_c": stat(2),
+                           "sampler": "every 100 ms over the timed region"}}
 
 
 def read_stages(ts, ctx):
@@ -368,6 +475,42 @@ def sharded_msm(ts, ctx, comm, pg, local, rank, world, reps=10):
             "msm_2^20_layout": f"2^20 pairs over {world} ranks, {cnt} per rank (tns_msm_sharded)"}
 
 
+class exchange_guard:
+    """A sharded step whose exchange fails (a peer rank stalled past the deadline, or the
+    transport broke) ends the run: one JSON line on stderr naming this rank, the step and the
+    communicator's diagnosis, then exit status 3 without waiting on the broken process group."""
+
+    def __init__(self, ts, rank, what):
+        self.ts, self.rank, self.what = ts, rank, what
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, et, e, tb):
+        if e is not None and isinstance(e, self.ts.DeviceError):
+            kind = "deadline" if isinstance(e, self.ts.ExchangeTimeout) else "transport"
+            print(json.dumps({"error": f"exchange {kind}", "rank": self.rank, "during": self.what,
+                              "detail": str(e)}), file=sys.stderr, flush=True)
+            os._exit(3)
+        return False
+
+
+def per_rank_exchange_record(pg, rank, dt, steps, s0, s1):
+    """Every rank's timed-region ms per step and its exchange steps' host latency over the timed
+    steps (tns_comm_stats deltas), gathered to every rank in rank order."""
+    n = s1["exchanges"] - s0["exchanges"]
+    tot = s1["total_s"] - s0["total_s"]
+    mine = {"rank": rank, "ms_per_step": round(dt / max(1, steps) * 1e3, 3),
+            "exchanges_per_step": round(n / max(1, steps), 2),
+            "mean_exchange_us": round(tot / n * 1e6, 1) if n else None,
+            "max_exchange_us_so_far": round(s1["max_us"], 1) if s1["max_us"] is not None else None}
+    if pg is None:
+        return [mine]
+    allv = [None] * pg.get_world_size()
+    pg.all_gather_object(allv, mine)
+    return allv
+
+
 def timed_proofs(fn, steps, warmup):
     for _ in range(warmup):
         fn()
@@ -420,12 +563,13 @@ def main():
         if args.comm == "rccl":
             uid = [ts.Comm.unique_id() if rank == 0 else None]
             pg.broadcast_object_list(uid, src=0)
-            comm = ts.Comm.rccl(ctx, rank, world, uid[0])
+            comm = ts.Comm.rccl(ctx, rank, world, uid[0], timeout_s=args.exchange_timeout)
         else:
             import torch
 
             on_gpu = torch.cuda.is_available() and not args.rehearse_one_gpu
-            comm = ts.Comm.torch(device=torch.device("cuda", local) if on_gpu else None)
+            comm = ts.Comm.torch(device=torch.device("cuda", local) if on_gpu else None,
+                                 timeout_s=args.exchange_timeout)
         # the rank count each transport itself reports must be --gpus (RCCL: ncclCommCount)
         info = comm.info()
         comm_cfg = {"kind": args.comm if args.comm == "rccl" else f"torch.distributed ({pg.get_backend()}) "
@@ -442,19 +586,27 @@ def main():
 
     def prove():
         if sharded:
-            return ts.twist_prove_sharded_resident(pp, comm, d_addr, d_val, d_isw, count, n_total)
+            with exchange_guard(ts, rank, "Twist::prove (sharded)"):
+                return ts.twist_prove_sharded_resident(pp, comm, d_addr, d_val, d_isw, count, n_total)
         return ts.twist_prove_resident(pp, d_addr, d_val, d_isw, n_ops)
 
     for _ in range(args.warmup):
         prove()
     barrier_sync(pg, local)
+    dstate = DeviceState(ts, local)
     ts.profile_enable(ctx, True)
     ts.profile_only(ctx, None if args.profile_all_timed else ROOF_KERNEL)
+    cs0 = comm.stats() if sharded else None
+    dstate.start()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         prove()
     barrier_sync(pg, local)
     dt = time.perf_counter() - t0
+    dstate.stop()
+    if sharded:
+        comm_cfg["per_rank"] = per_rank_exchange_record(pg, rank, dt, args.steps, cs0, comm.stats())
+        comm_cfg["exchange_timeout_s"] = args.exchange_timeout
     breakdown = ctx.timing()
     roof, stages = roofline_from_profile(ts, ctx)
     stage_steps = args.steps
@@ -496,6 +648,7 @@ def main():
         "twist_last_prove_ms": {k: round(v, 3) for k, v in breakdown.items()},
         "commit_basis": args.commit_basis,
         "setup_ms": {"setup_params": round(t_setup * 1e3, 1), "lagrange_basis": round(t_lag * 1e3, 1)},
+        "device_state": dstate.record(),
     }
     if rank == 0 and world == 1 and not args.no_extras:
         # drop-in rate: Twist::prove on host buffers through the C ABI (PCIe and host-side SoA
@@ -535,7 +688,8 @@ def main():
         out["shout_lookups_per_sec_2^20"] = round(T / t_sh, 1)
         out["shout_ms_2^20"] = round(t_sh * 1e3, 3)
     if sharded and not args.no_extras:  # the MSM half of the metric at N GPUs (C2 sharded)
-        out.update(sharded_msm(ts, ctx, comm, pg, local, rank, world))
+        with exchange_guard(ts, rank, "KZG MSM 2^20 (sharded)"):
+            out.update(sharded_msm(ts, ctx, comm, pg, local, rank, world))
     if rank == 0 and world == 1 and not args.no_extras and args.sumcheck_logs:
         out["sumcheck_generic"] = sumcheck_generic(ts, ctx, [int(x) for x in args.sumcheck_logs.split(",")])
     if roof is not None:

@@ -92,6 +92,21 @@ int tns_version(void);
 /* Number of visible HIP devices (0 if none); never fails. */
 int tns_device_count(void);
 
+/* Identity and clock ratings of one visible device (hipDeviceProp_t), recorded beside
+ * benchmark numbers so that a box's clocks can explain a difference between runs.  Not on
+ * the reference's path (bench.py's device-state record, src/benchmarks.rs:26-28). */
+typedef struct {
+  char name[64];          /* marketing name */
+  char arch[32];          /* gcnArchName, e.g. "gfx950:sramecc+:xnack-" */
+  char pci_bus_id[32];    /* "DDDD:BB:DD.F", the sysfs name of the device */
+  int32_t clock_khz;      /* peak shader clock (clockRate) */
+  int32_t mem_clock_khz;  /* peak memory clock (memoryClockRate) */
+  int32_t cu_count;       /* multiProcessorCount */
+  int32_t pad;
+  uint64_t total_mem;     /* bytes */
+} tns_device_info;
+int tns_device_info_get(int device, tns_device_info *out);
+
 /* ---------------------------------------------------------------- context */
 int tns_ctx_create(int device, tns_ctx **out);
 void tns_ctx_destroy(tns_ctx *ctx);
@@ -321,6 +336,14 @@ int tns_comm_info(const tns_comm *comm, int *rank, int *size, int *seen_size, in
 /* The communicator's allgather on its own (self-test / launcher use); ctx may be NULL for a
  * callback communicator. */
 int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv);
+/* Deadline of one exchange step (default 600 s).  RCCL: the collective is polled on the
+ * context stream and the communicator is aborted past the deadline; a host callback enforces
+ * its own deadline and returns non-zero.  Either way the prove call fails with TNS_ERR_DEVICE and
+ * a message naming this rank, the exchange step number and what it carried. */
+int tns_comm_set_timeout(tns_comm *comm, double seconds);
+/* out = {exchange steps so far, their total seconds, the longest one's seconds, the deadline}
+ * (multi-rank communicators; timed on the host around each allgather). */
+int tns_comm_stats(const tns_comm *comm, double out[4]);
 /* Build (and cache) rank `rank` of `size`'s slice of the Lagrange basis for N = 2^k nodes
  * ahead of the first sharded proof of that size (setup, like tns_srs_prepare_lagrange). */
 int tns_srs_prepare_lagrange_shard(tns_ctx *ctx, tns_srs *srs, size_t n, int rank, int size);
@@ -333,7 +356,11 @@ int tns_setup_params_shard(tns_ctx *ctx, unsigned log_size, int rank, int size, 
  * ranks (the C2 MSM at N GPUs): rank r holds coefficients [r N/size, r N/size + n_local) on the
  * device (N = next_pow2(n_total); n_local = that slice's length) and an SRS share covering them
  * (tns_setup_params_shard splits 2^k + 1 powers on those boundaries); one partial MSM per rank,
- * an allgather of the 96-byte partials.  Every rank returns the whole commitment. */
+ * an allgather of the 96-byte partials.  Every rank returns the whole commitment.
+ * Restriction: the slices must lie in the ranks' SRS shares, which follow the setup's 2^k
+ * boundaries, so next_pow2(n_total) must equal that 2^k (e.g. n_total = 2^20 over
+ * setup_params_shard(18)); any other n_total fails with TNS_ERR_INVALID_PARAMETERS (an unsharded
+ * tns_msm / tns_kzg_commit takes every length up to the SRS's). */
 int tns_msm_sharded(tns_ctx *ctx, const tns_srs *srs, tns_comm *comm, const uint64_t *d_scalars, size_t n_local,
                     uint64_t n_total, uint64_t out_proj[12]);
 /* Twist::prove of a trace of n_total operations whose operations

@@ -131,7 +131,7 @@ static G1Affine commit_evals(Ctx *c, const Srs &srs, EvalPoly &p, Comm &m) {
   p.basis = lagrange_basis_dev(c, srs, p.N, p.first, p.cnt);
   if (p.basis) {
     const G1Xyzz part = msm_dev(c, p.basis->points.as<G1Affine>(), p.y, p.cnt, p.basis->fb);
-    return xyzz_to_affine(allgather_sum_g1(c, m, part));
+    return xyzz_to_affine(allgather_sum_g1(c, m, part, "commitment partial MSM"));
   }
   if (m.size > 1) throw Error(TNS_ERR_INVALID_PARAMETERS, "sharded proving needs an SRS with tau (Lagrange basis)");
   if (p.N & (p.N - 1))
@@ -160,7 +160,7 @@ static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *val
       ell = part[0];
       S = part[1];
     } else {
-      const std::vector<Fr> all = allgather_fr(c, m, part, 2);
+      const std::vector<Fr> all = allgather_fr(c, m, part, 2, "barycentric partials");
       for (int r = 0; r < m.size; r++) {
         ell = mul(ell, all[2 * r]);
         S = add(S, all[2 * r + 1]);
@@ -169,7 +169,7 @@ static void open_evals(Ctx *c, const Srs &srs, EvalPoly &p, const Fr &z, Fr *val
     *value = mul(ell, S);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
     lagrange_quotient_finish_dev(c, p.y, p.cnt, *value, q);
     const G1Xyzz pp = msm_dev(c, p.basis->points.as<G1Affine>(), q, p.cnt, p.basis->fb);
-    *proof = xyzz_to_affine(allgather_sum_g1(c, m, pp));
+    *proof = xyzz_to_affine(allgather_sum_g1(c, m, pp, "opening partial MSM"));
     return;
   }
   if (m.size > 1)  // z on a node: probability ~2^-230; the coefficient route is unsharded
@@ -191,14 +191,14 @@ static G1Xyzz sum_rank_parts(const G1Xyzz *all, int size, int stride, int k) {
   return acc;
 }
 
-static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affine out[2]) {
+static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affine out[2], const char *what) {
   if (m.size == 1) {
     out[0] = xyzz_to_affine(part[0]);
     out[1] = xyzz_to_affine(part[1]);
     return;
   }
   std::vector<G1Xyzz> all(2 * (size_t)m.size);
-  m.allgather(c, part, 2 * sizeof(G1Xyzz), all.data());
+  m.exchange(c, part, 2 * sizeof(G1Xyzz), all.data(), what);
   out[0] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 0));
   out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 1));
 }
@@ -233,7 +233,7 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
   };
   G1Xyzz part[2];
   msm_pair_dev(c, args(p0, src0), args(p1, src1), part);
-  allgather_sum_g1_pair(c, m, part, out);
+  allgather_sum_g1_pair(c, m, part, out, "commitment pair partial MSMs");
 }
 
 // after_quotients (optional): called once the quotient kernel is queued (the side-stream folds'
@@ -268,7 +268,7 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
     lagrange_open_partial_dev(c, p1.y, p1.N, p1.first, p1.cnt, z, q1, &part[2], &part[3]);
   }
   Fr ell[2] = {Fr::one(), Fr::one()}, S[2] = {Fr::zero(), Fr::zero()};
-  const std::vector<Fr> all = allgather_fr(c, m, part, 4);
+  const std::vector<Fr> all = allgather_fr(c, m, part, 4, "barycentric pair partials");
   for (int r = 0; r < m.size; r++)
     for (int k = 0; k < 2; k++) {
       ell[k] = mul(ell[k], all[4 * (size_t)r + 2 * k]);
@@ -286,7 +286,7 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
   G1Xyzz pp[2];
   msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits},
                MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr}, pp);
-  allgather_sum_g1_pair(c, m, pp, proof);
+  allgather_sum_g1_pair(c, m, pp, proof, "opening pair partial MSMs");
 }
 
 // shard geometry: `size` ranks over N padded entries (size a power of two <= N)
@@ -330,6 +330,28 @@ int tns_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int tns_device_info_get(int device, tns_device_info *out) {
+  return guarded([&]() {
+    if (!out) throw Error(TNS_ERR_INVALID_PARAMETERS, "null output");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+      throw Error(TNS_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= n) throw Error(TNS_ERR_INVALID_PARAMETERS, "device index out of range");
+    hipDeviceProp_t p;
+    TNS_HIP(hipGetDeviceProperties(&p, device));
+    std::memset(out, 0, sizeof(*out));
+    std::snprintf(out->name, sizeof(out->name), "%s", p.name);
+    std::snprintf(out->arch, sizeof(out->arch), "%s", p.gcnArchName);
+    std::snprintf(out->pci_bus_id, sizeof(out->pci_bus_id), "%04x:%02x:%02x.0", p.pciDomainID, p.pciBusID,
+                  p.pciDeviceID);
+    out->clock_khz = p.clockRate;
+    out->mem_clock_khz = p.memoryClockRate;
+    out->cu_count = p.multiProcessorCount;
+    out->total_mem = p.totalGlobalMem;
+    return TNS_OK;
+  });
 }
 
 int tns_ctx_create(int device, tns_ctx **out) {
@@ -476,6 +498,8 @@ int tns_srs_download(tns_ctx *ctx, const tns_srs *srs, uint64_t *g1_out, size_t 
 int tns_srs_download_indices(tns_ctx *ctx, const tns_srs *srs, const uint64_t *idx, size_t k,
                              uint64_t *g1_out) {
   return guarded([&]() {
+    if (!ctx || !srs) throw Error(TNS_ERR_INVALID_PARAMETERS, "null context or SRS");
+    if (k > 0 && (!idx || !g1_out)) throw Error(TNS_ERR_INVALID_PARAMETERS, "null index or output buffer");
     CtxScope g(&ctx->c);
     for (size_t t = 0; t < k; t++)
       if (idx[t] < srs->s.first || idx[t] >= srs->s.first + srs->s.held)
@@ -490,10 +514,12 @@ int tns_srs_download_indices(tns_ctx *ctx, const tns_srs *srs, const uint64_t *i
 }
 
 int tns_srs_share(const tns_srs *srs, uint64_t *first, uint64_t *held) {
-  if (!srs) return TNS_ERR_INVALID_PARAMETERS;
-  *first = srs->s.first;
-  *held = srs->s.held;
-  return TNS_OK;
+  return guarded([&]() {
+    if (!srs || !first || !held) throw Error(TNS_ERR_INVALID_PARAMETERS, "null SRS or output");
+    *first = srs->s.first;
+    *held = srs->s.held;
+    return TNS_OK;
+  });
 }
 
 size_t tns_srs_len(const tns_srs *srs) { return srs ? srs->s.n : 0; }
@@ -945,7 +971,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   Fr finals[3];
   for (int j = 0; j < n_mles; j++) finals[j] = vals[j];
   if (lr) {
-    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles);  // rank-major
+    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles, "sum-check folded table values");  // rank-major
     for (int j = 0; j < n_mles; j++) {
       std::vector<Fr> t(m.size);
       for (int r = 0; r < m.size; r++) t[r] = all[(size_t)r * n_mles + j];
@@ -1244,7 +1270,7 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   }
   if (m.size > 1) {
     std::vector<unsigned> flags(m.size);
-    m.allgather(c, &hbad, sizeof hbad, flags.data());
+    m.exchange(c, &hbad, sizeof hbad, flags.data(), "input validity flags");
     for (unsigned f : flags) hbad |= f;
   }
   if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
@@ -1611,7 +1637,28 @@ int tns_comm_info(const tns_comm *comm, int *rank, int *size, int *seen_size, in
 int tns_comm_allgather(tns_ctx *ctx, tns_comm *comm, const void *send, size_t bytes, void *recv) {
   return guarded([&]() {
     if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
-    comm->c->allgather(ctx ? &ctx->c : nullptr, send, bytes, recv);
+    if (bytes && (!send || !recv)) throw Error(TNS_ERR_INVALID_PARAMETERS, "null exchange buffer");
+    comm->c->exchange(ctx ? &ctx->c : nullptr, send, bytes, recv, "tns_comm_allgather");
+    return TNS_OK;
+  });
+}
+
+int tns_comm_set_timeout(tns_comm *comm, double seconds) {
+  return guarded([&]() {
+    if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
+    if (!(seconds > 0.0)) throw Error(TNS_ERR_INVALID_PARAMETERS, "timeout must be positive");
+    comm->c->timeout_s = seconds;
+    return TNS_OK;
+  });
+}
+
+int tns_comm_stats(const tns_comm *comm, double out[4]) {
+  return guarded([&]() {
+    if (!comm || !comm->c || !out) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator or output");
+    out[0] = (double)comm->c->seq;
+    out[1] = comm->c->total_s;
+    out[2] = comm->c->max_s;
+    out[3] = comm->c->timeout_s;
     return TNS_OK;
   });
 }
@@ -1692,7 +1739,7 @@ int tns_msm_sharded(tns_ctx *ctx, const tns_srs *srs, tns_comm *comm, const uint
     const G1Xyzz part = n_local ? msm_dev(&ctx->c, srs->s.points.as<G1Affine>() + off, (const Fr *)d_scalars, n_local,
                                           fb, off)
                                 : G1Xyzz::inf();
-    store_proj(xyzz_to_affine(allgather_sum_g1(&ctx->c, m, part)), out);
+    store_proj(xyzz_to_affine(allgather_sum_g1(&ctx->c, m, part, "sharded MSM partial")), out);
     return TNS_OK;
   });
 }

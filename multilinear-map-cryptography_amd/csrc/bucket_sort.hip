@@ -882,11 +882,19 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   int shift = keybits - bits[0];
 
   // pass 1: scalars -> bins of the top bits[0] key bits
+  const bool runtime_pass1 = getenv("TNS_BS_RUNTIME_PASS1") != nullptr;  // (A/B: the runtime-plan kernels)
+  if (J.corun) {  // the small-register co-run kernels exist only as compile-time plans
+    bool have = false;
+    if (!runtime_pass1)
+      for (const Pass1Plan &p : kPass1Plans) have |= p.corun && p.tile == BS_CORUN_TILE && p.c == c && p.W == W;
+    if (!have) J.corun = false;  // full-size kernels instead (same result, no co-residence)
+  }
   const int tile1 = J.corun ? BS_CORUN_TILE : W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
   const Pass1Plan *ct = nullptr;
-  if (!getenv("TNS_BS_RUNTIME_PASS1"))  // (A/B: the runtime-plan kernels)
+  if (!runtime_pass1)
     for (const Pass1Plan &p : kPass1Plans)
       if (p.tile == tile1 && p.c == c && p.W == W && p.corun == J.corun) ct = &p;
+  if ((size_t)tile1 < (size_t)W) throw Error(TNS_ERR_INVALID_PARAMETERS, "bucket sort: more windows than a pass-1 tile holds");
   A.spb = (size_t)tile1 / W;
   if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
   const size_t T1 = (n + A.spb - 1) / A.spb;

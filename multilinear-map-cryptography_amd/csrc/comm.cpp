@@ -13,8 +13,10 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.hpp"
@@ -53,16 +55,39 @@ struct RcclComm final : Comm {
   int kind() const override { return 2; }
   int seen_size() const override {
     int n = 0;
+    if (!comm) throw Error(TNS_ERR_DEVICE, "RCCL communicator was aborted by an earlier timeout");
     TNS_NCCL(ncclCommCount(comm, &n));
     return n;
   }
   void allgather(Ctx *c, const void *send, size_t bytes, void *recv) override {
     if (!c) throw Error(TNS_ERR_INVALID_PARAMETERS, "the RCCL communicator needs a context");
+    if (!comm) throw Error(TNS_ERR_DEVICE, "RCCL communicator was aborted by an earlier timeout");
     void *ds = send_b.ensure(bytes ? bytes : 1), *dr = recv_b.ensure(bytes * size ? bytes * size : 1);
     TNS_HIP(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, c->stream));
     TNS_NCCL(ncclAllGather(ds, dr, bytes, ncclUint8, comm, c->stream));
     TNS_HIP(hipMemcpyAsync(recv, dr, bytes * size, hipMemcpyDeviceToHost, c->stream));
-    TNS_HIP(hipStreamSynchronize(c->stream));
+    // wait with a deadline: a rank that never joins leaves the collective pending forever, so
+    // poll the stream (and RCCL's own async error) and abort the communicator past timeout_s
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 0;; spin++) {
+      hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) TNS_HIP(q);
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+        (void)ncclCommAbort(comm);
+        comm = nullptr;
+        throw Error(TNS_ERR_DEVICE, std::string("RCCL allgather failed: ") + ncclGetErrorString(ae));
+      }
+      const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (el > timeout_s) {
+        (void)ncclCommAbort(comm);  // releases the pending collective; the communicator is dead
+        comm = nullptr;
+        throw Error(TNS_ERR_DEVICE, "RCCL allgather timed out after " + std::to_string(el) +
+                                        " s (a peer rank never joined; communicator aborted)");
+      }
+      if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
   }
 };
 
@@ -107,19 +132,38 @@ Comm *comm_rccl_new(Ctx *c, int rank, int size, const uint8_t uid[128]) {
   return r;
 }
 
+void Comm::exchange(Ctx *c, const void *send, size_t bytes, void *recv, const char *what) {
+  if (size == 1) {  // the shared one-rank communicator: no counters (used from many threads)
+    allgather(c, send, bytes, recv);
+    return;
+  }
+  const uint64_t step = ++seq;
+  const auto t0 = std::chrono::steady_clock::now();
+  try {
+    allgather(c, send, bytes, recv);
+  } catch (const Error &e) {
+    throw Error(e.code, "rank " + std::to_string(rank) + " of " + std::to_string(size) + ": exchange #" +
+                            std::to_string(step) + " (" + (what ? what : "?") + ", " + std::to_string(bytes) +
+                            " B per rank): " + e.what());
+  }
+  const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  total_s += el;
+  if (el > max_s) max_s = el;
+}
+
 // ---------------------------------------------------------------- combined exchanges
-G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part) {
+G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part, const char *what) {
   if (m.size == 1) return part;
   std::vector<G1Xyzz> all(m.size);
-  m.allgather(c, &part, sizeof part, all.data());
+  m.exchange(c, &part, sizeof part, all.data(), what);
   G1Xyzz acc = G1Xyzz::inf();
   for (const auto &p : all) acc = xyzz_add(acc, p);
   return acc;
 }
 
-std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k) {
+std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k, const char *what) {
   std::vector<Fr> all(k * m.size);
-  m.allgather(c, part, sizeof(Fr) * k, all.data());
+  m.exchange(c, part, sizeof(Fr) * k, all.data(), what);
   return all;
 }
 

@@ -584,6 +584,11 @@ const LagrangeBasis *lagrange_basis_from_powers_dev(Ctx *c, const Srs &srs, size
 // comm.cpp: the exchange steps of a sharded proof
 struct Comm {
   int rank = 0, size = 1;
+  // deadline of one exchange (RCCL: polled on the stream, then ncclCommAbort; a host callback
+  // enforces its own and returns non-zero), exchange counter and latency statistics
+  double timeout_s = 600.0;
+  uint64_t seq = 0;
+  double total_s = 0.0, max_s = 0.0;
   virtual ~Comm() = default;
   // 0 = one rank (self), 1 = host callback, 2 = RCCL
   virtual int kind() const = 0;
@@ -591,13 +596,15 @@ struct Comm {
   virtual int seen_size() const { return size; }
   // every rank's `bytes` from `send`, in rank order, into recv (size * bytes)
   virtual void allgather(Ctx *c, const void *send, size_t bytes, void *recv) = 0;
+  // one numbered, timed exchange step; a failure names this rank, the step and `what`
+  void exchange(Ctx *c, const void *send, size_t bytes, void *recv, const char *what);
 };
 Comm &comm_self();
 Comm *comm_callback_new(int rank, int size, tns_allgather_fn fn, void *user);
 Comm *comm_rccl_new(Ctx *c, int rank, int size, const uint8_t uid[128]);
 void comm_unique_id(uint8_t out[128]);
-G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part);
-std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k);
+G1Xyzz allgather_sum_g1(Ctx *c, Comm &m, const G1Xyzz &part, const char *what);
+std::vector<Fr> allgather_fr(Ctx *c, Comm &m, const Fr *part, size_t k, const char *what);
 
 // pairing.cpp: BN254 G2 (D-type twist, affine over Fq2 = Fq[u]/(u^2+1)) and the pairing
 struct G2Affine {

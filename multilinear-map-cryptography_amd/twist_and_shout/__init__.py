@@ -189,6 +189,15 @@ def device_count() -> int:
     return N.load().tns_device_count()
 
 
+def device_info(device: int = 0) -> dict:
+    """hipDeviceProp_t identity and clock ratings of one visible device (tns_device_info_get)."""
+    info = N.TnsDeviceInfo()
+    _check(N.load().tns_device_info_get(device, C.byref(info)))
+    return {"name": info.name.decode(errors="replace"), "arch": info.arch.decode(errors="replace"),
+            "pci_bus_id": info.pci_bus_id.decode(errors="replace"), "clock_khz": info.clock_khz,
+            "mem_clock_khz": info.mem_clock_khz, "cu_count": info.cu_count, "total_mem": info.total_mem}
+
+
 # ----------------------------------------------------------------------------- params
 class Srs:
     """Device-resident CommitmentParams.g1_powers."""
@@ -1201,12 +1210,31 @@ def msm_resident(params: CommitmentParams, scalars: DeviceBuffer, n: int) -> np.
 _AllgatherFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
 
 
+class ExchangeTimeout(DeviceError):
+    """An exchange step of a sharded proof passed its deadline (a peer rank stalled or died)."""
+
+
 class Comm:
     """Communicator of one sharded proof (tns_comm): the allgathers of partial MSM sums,
-    barycentric partials and folded table values."""
+    barycentric partials and folded table values.
 
-    def __init__(self, handle: C.c_void_p, rank: int, size: int, keep=None):
+    Every exchange step has a deadline (`timeout_s`, default 600 s): the RCCL transport polls its
+    collective and aborts the communicator, a host-callback transport enforces it in the
+    callback.  A step that misses it fails the prove call with a message naming this rank, the
+    step number and what it carried -- and, for the torch transport, the last step every peer
+    rank reached (from the process group's store), i.e. which rank stalled."""
+
+    DEFAULT_TIMEOUT_S = 600.0
+
+    def __init__(self, handle: C.c_void_p, rank: int, size: int, keep=None, timeout_s: Optional[float] = None):
         self.handle, self.rank, self.size, self._keep = handle, rank, size, keep
+        self.last_failure: Optional[str] = None
+        self.timeout_s = float(timeout_s or self.DEFAULT_TIMEOUT_S)
+        _check(N.load().tns_comm_set_timeout(self.handle, self.timeout_s))
+
+    def set_timeout(self, seconds: float):
+        _check(N.load().tns_comm_set_timeout(self.handle, float(seconds)))
+        self.timeout_s = float(seconds)
 
     @staticmethod
     def unique_id() -> bytes:
@@ -1215,46 +1243,101 @@ class Comm:
         return bytes(buf)
 
     @classmethod
-    def rccl(cls, ctx: Context, rank: int, size: int, uid: bytes) -> "Comm":
+    def rccl(cls, ctx: Context, rank: int, size: int, uid: bytes, timeout_s: Optional[float] = None) -> "Comm":
         """RCCL communicator (ncclAllGather over xGMI); uid from Comm.unique_id() on rank 0."""
         h = C.c_void_p()
         _check(N.load().tns_comm_create(ctx.handle, rank, size, (C.c_uint8 * 128)(*uid), C.byref(h)))
-        return cls(h, rank, size)
+        return cls(h, rank, size, timeout_s=timeout_s)
 
     @classmethod
-    def from_allgather(cls, rank: int, size: int, fn) -> "Comm":
-        """fn(local: bytes) -> bytes: every rank's bytes concatenated in rank order."""
+    def from_allgather(cls, rank: int, size: int, fn, timeout_s: Optional[float] = None) -> "Comm":
+        """fn(local: bytes) -> bytes: every rank's bytes concatenated in rank order.  fn may take
+        a keyword `deadline_s` (the communicator's deadline) and should raise past it."""
+        holder = {}
+
         def cb(user, send, nbytes, recv):
+            me = holder.get("comm")
             try:
-                out = fn(C.string_at(send, nbytes))
+                out = fn(C.string_at(send, nbytes), **({"deadline_s": me.timeout_s} if holder.get("kw") else {}))
                 if len(out) != nbytes * size:
+                    if me is not None:
+                        me.last_failure = f"allgather returned {len(out)} bytes, expected {nbytes * size}"
                     return 2
                 C.memmove(recv, out, len(out))
                 return 0
-            except Exception:  # noqa: BLE001 -- reported to the library as a failed exchange
-                return 1
+            except Exception as e:  # noqa: BLE001 -- reported to the library as a failed exchange
+                if me is not None:
+                    me.last_failure = f"{type(e).__name__}: {e}"
+                return 3 if isinstance(e, TimeoutError) else 1
+        import inspect
+
+        try:
+            holder["kw"] = "deadline_s" in inspect.signature(fn).parameters
+        except (TypeError, ValueError):
+            holder["kw"] = False
         cfn = _AllgatherFn(cb)
         h = C.c_void_p()
         _check(N.load().tns_comm_create_callback(rank, size, C.cast(cfn, C.c_void_p), None, C.byref(h)))
-        return cls(h, rank, size, keep=cfn)
+        comm = cls(h, rank, size, keep=cfn, timeout_s=timeout_s)
+        holder["comm"] = comm
+        return comm
 
     @classmethod
-    def torch(cls, group=None, device=None) -> "Comm":
+    def torch(cls, group=None, device=None, timeout_s: Optional[float] = None) -> "Comm":
         """Allgather through an initialised torch.distributed process group (nccl = RCCL on
-        ROCm, or gloo)."""
+        ROCm, or gloo), with a deadline per step: the collective is issued asynchronously and
+        polled; before it each rank publishes its step number in the group's store, so a rank
+        whose step passes the deadline reports which peers never reached that step."""
         import torch
         import torch.distributed as dist
 
         rank, size = dist.get_rank(group), dist.get_world_size(group)
+        try:
+            from torch.distributed import distributed_c10d as c10d
 
-        def fn(data: bytes) -> bytes:
+            store = c10d._get_default_store()
+        except Exception:  # noqa: BLE001 -- diagnostics only
+            store = None
+        state = {"step": 0}
+
+        def peers_behind(step):
+            if store is None:
+                return "peer steps unknown (no process-group store)"
+            seen = []
+            for r in range(size):
+                key = f"tns_comm/step/{r}"
+                try:
+                    v = int(store.get(key)) if store.check([key]) else 0
+                except Exception:  # noqa: BLE001
+                    v = -1
+                seen.append(v)
+            late = [r for r, v in enumerate(seen) if v < step]
+            return f"peer ranks still before step {step}: {late} (last step per rank: {seen})"
+
+        def fn(data: bytes, deadline_s: float = cls.DEFAULT_TIMEOUT_S) -> bytes:
+            import time as _time
+
+            state["step"] += 1
+            step = state["step"]
+            if store is not None:
+                try:
+                    store.set(f"tns_comm/step/{rank}", str(step))
+                except Exception:  # noqa: BLE001
+                    pass
             t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
             if device is not None:
                 t = t.to(device)
             out = torch.empty(len(data) * size, dtype=torch.uint8, device=t.device)
-            dist.all_gather_into_tensor(out, t, group=group)
+            work = dist.all_gather_into_tensor(out, t, group=group, async_op=True)
+            t0 = _time.monotonic()
+            while not work.is_completed():
+                if _time.monotonic() - t0 > deadline_s:
+                    raise TimeoutError(f"rank {rank}: allgather step {step} ({len(data)} B) passed its "
+                                       f"{deadline_s:g} s deadline; {peers_behind(step)}")
+                _time.sleep(0.0002)
+            work.wait()
             return out.cpu().numpy().tobytes()
-        return cls.from_allgather(rank, size, fn)
+        return cls.from_allgather(rank, size, fn, timeout_s=timeout_s)
 
     KINDS = {0: "self", 1: "callback", 2: "rccl"}
 
@@ -1264,14 +1347,36 @@ class Comm:
         _check(N.load().tns_comm_info(self.handle, C.byref(r), C.byref(n), C.byref(seen), C.byref(k)))
         return {"rank": r.value, "size": n.value, "seen_size": seen.value, "kind": self.KINDS.get(k.value, "?")}
 
+    def stats(self) -> dict:
+        """Exchange steps so far and their host-timed latency (tns_comm_stats)."""
+        out = (C.c_double * 4)()
+        _check(N.load().tns_comm_stats(self.handle, out))
+        n = int(out[0])
+        return {"exchanges": n, "total_s": out[1], "mean_us": (out[1] / n * 1e6) if n else None,
+                "max_us": out[2] * 1e6 if n else None, "timeout_s": out[3]}
+
     def allgather(self, data: bytes, ctx: Optional[Context] = None) -> bytes:
         """The communicator's own allgather (every rank's bytes, in rank order)."""
         src = (C.c_uint8 * max(1, len(data))).from_buffer_copy(data or b"\0")
         out = (C.c_uint8 * max(1, len(data) * self.size))()
-        _check(N.load().tns_comm_allgather(ctx.handle if ctx else None, self.handle, src, len(data), out))
+        self.check(N.load().tns_comm_allgather(ctx.handle if ctx else None, self.handle, src, len(data), out))
         return bytes(out)[:len(data) * self.size]
 
+    def check(self, status: int):
+        """_check for a call that exchanged through this communicator: a failed exchange step
+        raises ExchangeTimeout (deadline) or DeviceError with the transport's own diagnosis."""
+        if status == 0:
+            return
+        msg = f"[{N.STATUS_NAMES.get(status, status)}] {N.last_error()}"
+        if self.last_failure:
+            msg += f" -- {self.last_failure}"
+        if "timed out" in msg or "deadline" in msg:
+            raise ExchangeTimeout(msg)
+        raise _ERRORS.get(status, DeviceError)(msg)
+
     def __del__(self):
+        if _EXITING:  # interpreter shutdown: RCCL / HIP may already be torn down (as Context.__del__)
+            return
         try:
             N.load().tns_comm_destroy(self.handle)
         except Exception:
@@ -1308,7 +1413,7 @@ def msm_sharded_resident(params: CommitmentParams, comm: Comm, scalars: DeviceBu
     Returns the commitment's projective limbs (every rank the same)."""
     srs = params.srs
     out = np.zeros(12, dtype=np.uint64)
-    _check(N.load().tns_msm_sharded(srs.ctx.handle, srs.handle, comm.handle, scalars.ptr, n_local, n_total,
+    comm.check(N.load().tns_msm_sharded(srs.ctx.handle, srs.handle, comm.handle, scalars.ptr, n_local, n_total,
                                     N.p64(out)))
     return out
 
@@ -1317,7 +1422,7 @@ def twist_prove_sharded_resident(pp: ProverParams, comm: Comm, addr: DeviceBuffe
                                  is_write: DeviceBuffer, n_local: int, n_total: int) -> N.TnsProof:
     srs = pp.commitment_params.srs
     pr = N.TnsProof()
-    _check(N.load().tns_twist_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, addr.ptr,
+    comm.check(N.load().tns_twist_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, addr.ptr,
                                             value.ptr, is_write.ptr, n_local, n_total, C.byref(pr)))
     return pr
 
@@ -1327,7 +1432,7 @@ def shout_prove_sharded_resident(pp: ProverParams, comm: Comm, entries: DeviceBu
                                  n_lookups_total: int) -> N.TnsProof:
     srs = pp.commitment_params.srs
     pr = N.TnsProof()
-    _check(N.load().tns_shout_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, entries.ptr,
+    comm.check(N.load().tns_shout_prove_sharded(srs.ctx.handle, srs.handle, C.byref(pp.raw()), comm.handle, entries.ptr,
                                             n_entries, n_entries_total, indices.ptr, n_lookups, n_lookups_total,
                                             C.byref(pr)))
     return pr

@@ -58,6 +58,12 @@ class TnsProof(C.Structure):
     ]
 
 
+class TnsDeviceInfo(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("arch", C.c_char * 32), ("pci_bus_id", C.c_char * 32),
+                ("clock_khz", C.c_int32), ("mem_clock_khz", C.c_int32), ("cu_count", C.c_int32),
+                ("pad", C.c_int32), ("total_mem", C.c_uint64)]
+
+
 class TnsTerm(C.Structure):
     _fields_ = [("coeff", C.c_uint64 * 4), ("tables", C.c_int32 * 3), ("pad", C.c_int32)]
 
@@ -71,6 +77,7 @@ SIGNATURES = [
     ("tns_last_error", C.c_char_p, []),
     ("tns_version", C.c_int, []),
     ("tns_device_count", C.c_int, []),
+    ("tns_device_info_get", C.c_int, [C.c_int, C.POINTER(TnsDeviceInfo)]),
     ("tns_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
     ("tns_ctx_destroy", None, [C.c_void_p]),
     ("tns_ctx_synchronize", C.c_int, [C.c_void_p]),
@@ -157,6 +164,8 @@ SIGNATURES = [
                                 C.POINTER(C.c_int)]),
     ("tns_msm_sharded", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint64, U64P]),
     ("tns_comm_allgather", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
+    ("tns_comm_set_timeout", C.c_int, [C.c_void_p, C.c_double]),
+    ("tns_comm_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     ("tns_srs_prepare_lagrange_shard", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]),
     ("tns_setup_params_shard", C.c_int,
      [C.c_void_p, C.c_uint, C.c_int, C.c_int, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),

@@ -146,3 +146,29 @@ def test_mle_table_follows_reference_struct():
     m = ts.MultilinearExtension(1, [1, 2, 3, 4, 5])  # long: entry i counts at i mod 2
     assert ts.from_mont(m._table()) == [1 + 3 + 5, 2 + 4]
     assert ts.from_mont(ts.MultilinearExtension(0, [])._table()) == [0]
+
+
+def test_null_arguments_are_invalid_parameters():
+    """Entry points handed NULL return TNS_ERR_INVALID_PARAMETERS instead of dereferencing it
+    (a C or Rust caller's NULL must not crash the process)."""
+    lib = N.load()
+    first, held = C.c_uint64(), C.c_uint64()
+    assert lib.tns_srs_share(None, C.byref(first), C.byref(held)) == 1
+    idx = np.zeros(1, dtype=np.uint64)
+    out = np.zeros(8, dtype=np.uint64)
+    assert lib.tns_srs_download_indices(None, None, N.p64(idx), 1, N.p64(out)) == 1
+    assert lib.tns_comm_set_timeout(None, 1.0) == 1
+    assert lib.tns_comm_stats(None, (C.c_double * 4)()) == 1
+    assert lib.tns_device_info_get(0, None) in (1, 101)
+
+
+def test_comm_timeout_and_stats_abi():
+    """A one-rank callback communicator: deadline setter validation and the stats record."""
+    lib = N.load()
+    comm = ts.Comm.from_allgather(0, 1, lambda b: b, timeout_s=2.5)
+    assert comm.stats() == {"exchanges": 0, "total_s": 0.0, "mean_us": None, "max_us": None, "timeout_s": 2.5}
+    assert lib.tns_comm_set_timeout(comm.handle, 0.0) == 1
+    assert lib.tns_comm_set_timeout(comm.handle, -1.0) == 1
+    comm.set_timeout(7.0)
+    assert comm.allgather(b"abc") == b"abc"
+    assert comm.stats()["timeout_s"] == 7.0

@@ -74,6 +74,57 @@ def _comm_body(rank, world):
     return got
 
 
+def _deadline_body(rank, world):
+    """Rank 1 joins the second exchange step 3 s late: rank 0's step passes its 1.5 s deadline
+    and fails naming itself, the step and the peer that never reached it; the late collective
+    then completes once rank 1 joins (no rank is left hanging)."""
+    import time
+
+    import twist_and_shout as ts
+
+    comm = ts.Comm.torch(timeout_s=1.5)
+    assert comm.stats()["timeout_s"] == 1.5
+    assert comm.allgather(bytes([rank]) * 8) == bytes([0]) * 8 + bytes([1]) * 8
+    if rank == 0:
+        t0 = time.monotonic()
+        with pytest.raises(ts.ExchangeTimeout) as ei:
+            comm.allgather(b"late")
+        waited = time.monotonic() - t0
+        msg = str(ei.value)
+        assert 1.4 < waited < 2.9, waited
+        assert "rank 0 of 2: exchange #2" in msg, msg
+        assert "peer ranks still before step 2: [1]" in msg, msg
+        st = comm.stats()
+        assert st["exchanges"] == 2 and st["max_us"] is not None
+        return msg
+    time.sleep(3.0)
+    comm.allgather(b"late")  # completes rank 0's abandoned collective
+    return comm.stats()["exchanges"]
+
+
+def _exit_entry(rank, world, port, errfile):
+    """bench.exchange_guard's exit path: rank 0's first exchange misses its deadline because
+    rank 1 never joins; rank 0 must exit with status 3 and one JSON line naming rank and step."""
+    for p in (ROOT, os.path.join(ROOT, "multilinear-map-cryptography_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import time
+
+    import bench
+    import twist_and_shout as ts
+
+    comm = ts.Comm.torch(timeout_s=1.0)
+    if rank == 1:
+        time.sleep(4.0)
+        os._exit(0)
+    sys.stderr = open(errfile, "w")
+    with bench.exchange_guard(ts, rank, "test exchange"):
+        comm.allgather(b"x" * 32)
+    os._exit(0)  # not reached: the guard exits with status 3
+
+
 def _bench_helpers_body(rank, world):
     import bench
 
@@ -211,3 +262,28 @@ def test_shard_geometry_and_trace_slices_gloo():
 @pytest.mark.timeout(600)
 def test_sharded_protocol_algebra_on_oracle_gloo():
     assert _run(_protocol_body) == [0, 1]
+
+
+@pytest.mark.timeout(600)
+def test_exchange_deadline_names_rank_and_step_gloo():
+    outs = _run(_deadline_body)
+    assert "deadline" in outs[0] and outs[1] == 2
+
+
+@pytest.mark.timeout(600)
+def test_exchange_deadline_exits_nonzero_gloo(tmp_path):
+    import json
+
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    errfile = str(tmp_path / "rank0.err")
+    procs = [ctx.Process(target=_exit_entry, args=(r, 2, port, errfile)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert procs[0].exitcode == 3, procs[0].exitcode
+    assert procs[1].exitcode == 0
+    rec = json.loads(open(errfile).read().strip().splitlines()[-1])
+    assert rec["error"] == "exchange deadline" and rec["rank"] == 0 and rec["during"] == "test exchange"
+    assert "exchange #1" in rec["detail"] and "peer ranks still before step 1: [1]" in rec["detail"]

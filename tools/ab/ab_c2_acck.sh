@@ -1,5 +1,5 @@
 #!/bin/bash
-# C2 (2^20 MSM) per accumulation chunk size: tools/ab_c2_acck.sh 32 64 70 ...
+# C2 (2^20 MSM) per accumulation chunk size: tools/ab/ab_c2_acck.sh 32 64 70 ...
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for k in "$@"; do

@@ -1,5 +1,5 @@
 #!/bin/bash
-# C2 (2^20 full-width MSM) reduction-shape A/B: tools/ab_c2red.sh "VAR=a VAR2=b" ...
+# C2 (2^20 full-width MSM) reduction-shape A/B: tools/ab/ab_c2red.sh "VAR=a VAR2=b" ...
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 for rep in 1 2; do

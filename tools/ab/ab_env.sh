@@ -1,5 +1,5 @@
 #!/bin/bash
-# C4 bench under several environment settings: tools/ab_env.sh "VAR=a" "VAR=b" ...
+# C4 bench under several environment settings: tools/ab/ab_env.sh "VAR=a" "VAR=b" ...
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 i=0

@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of library builds on the GPU box: tools/ab_lib.sh <log_n> <tag>...  (tag "lib" = libtns.so,
+# A/B of library builds on the GPU box: tools/ab/ab_lib.sh <log_n> <tag>...  (tag "lib" = libtns.so,
 # else multilinear-map-cryptography_amd/libtns_<tag>.so); standalone MSM 2^log_n then one C4 bench line each
 set -euo pipefail
 k=$1; shift

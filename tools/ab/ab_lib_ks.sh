@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of library builds with kernel traces: tools/ab_lib_ks.sh <log_n> <tag>...  (tag "lib" = libtns.so,
+# A/B of library builds with kernel traces: tools/ab/ab_lib_ks.sh <log_n> <tag>...  (tag "lib" = libtns.so,
 # else multilinear-map-cryptography_amd/libtns_<tag>.so): the last standalone 2^log_n MSM's kernels, then
 # one C4 bench line (ms/step and per-stage device time) per build
 set -euo pipefail

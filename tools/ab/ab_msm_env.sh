@@ -1,5 +1,5 @@
 #!/bin/bash
-# standalone 2^k MSM kernel traces under env settings: tools/ab_msm_env.sh <tag> <log_n> "VAR=a VAR2=b" ...
+# standalone 2^k MSM kernel traces under env settings: tools/ab/ab_msm_env.sh <tag> <log_n> "VAR=a VAR2=b" ...
 # prints the per-kernel durations of the last MSM of each setting
 set -euo pipefail
 tag=$1; k=$2; shift 2

@@ -5,7 +5,7 @@ set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "msm or MSM or sort or lagrange or twist or shout" > gpurun_out/p1p_pytest.log 2>&1
 tail -2 gpurun_out/p1p_pytest.log
-bash tools/ab_env.sh "TNS_NONE=0" "TNS_BS_P1_BLOCKS=0" "TNS_NONE=0" "TNS_BS_P1_BLOCKS=0"
+bash tools/ab/ab_env.sh "TNS_NONE=0" "TNS_BS_P1_BLOCKS=0" "TNS_NONE=0" "TNS_BS_P1_BLOCKS=0"
 for e in "TNS_NONE=0" "TNS_BS_P1_BLOCKS=0"; do
   for k in 20 24; do env $e timeout -k 10 120 python -u tools/msm_trace.py $k 10 | sed "s/^/$e /"; done
 done

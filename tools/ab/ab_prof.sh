@@ -1,6 +1,6 @@
 #!/bin/bash
 # timed-region profiling A/B: only the roofline kernel timed (default) vs every stage timed
-# inside the timed steps (--profile-all-timed).  tools/ab_prof.sh
+# inside the timed steps (--profile-all-timed).  tools/ab/ab_prof.sh
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 i=0

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call: parity tests, the default bench line, and a rocprofv3 kernel-trace summary.
-#   tools/gpu_round.sh <tag>
+#   tools/ab/gpu_round.sh <tag>
 set -euo pipefail
 tag=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -2,7 +2,7 @@
 # Run GPU steps in order; each is "name|timeout_s|command".  A step that fails with an ordinary
 # test/script failure (exit 1 or 2) lets the next step run; anything else (a fault, abort,
 # segfault, time limit: 124/134/137/139...) stops the sequence -- no further GPU work after it.
-# Usage: tools/gpu_steps.sh "tests|300|python -u -m pytest ..." "bench|560|python -u bench.py ..."
+# Usage: tools/ab/gpu_steps.sh "tests|300|python -u -m pytest ..." "bench|560|python -u bench.py ..."
 mkdir -p gpurun_out
 for step in "$@"; do
   name="${step%%|*}"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# kernel trace of a short C4 bench under an environment setting: tools/ks_env.sh <tag> [VAR=val ...]
+# kernel trace of a short C4 bench under an environment setting: tools/ab/ks_env.sh <tag> [VAR=val ...]
 set -euo pipefail
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out

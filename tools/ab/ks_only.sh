@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 kernel trace + stats of a short C4 bench: tools/ks_only.sh <tag> [bench args...]
+# rocprofv3 kernel trace + stats of a short C4 bench: tools/ab/ks_only.sh <tag> [bench args...]
 set -euo pipefail
 tag=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -1,5 +1,5 @@
 #!/bin/bash
-# standalone MSM timing under env settings: tools/msm_env.sh <log_n> "VAR=a" "VAR=b" ...
+# standalone MSM timing under env settings: tools/ab/msm_env.sh <log_n> "VAR=a" "VAR=b" ...
 set -euo pipefail
 k=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out

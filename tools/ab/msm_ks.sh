@@ -1,5 +1,5 @@
 #!/bin/bash
-# kernel trace of standalone MSMs: tools/msm_ks.sh <tag> <log_n> [VAR=val ...]
+# kernel trace of standalone MSMs: tools/ab/msm_ks.sh <tag> <log_n> [VAR=val ...]
 set -euo pipefail
 tag=$1; k=$2; shift 2
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out

@@ -10,4 +10,4 @@ if [ -n "${TESTS:-}" ]; then
 TNS_MSM_STAGGER=1 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$TESTS" > $out/pytest.log 2>&1
 rc=$?; tail -3 $out/pytest.log; [ $rc = 0 ] || { grep -E "Error|assert|FAILED" $out/pytest.log | head -20; exit $rc; }
 fi
-AB="${AB:--;TNS_MSM_STAGGER=1;TNS_MSM_STAGGER=1 TNS_ACC_WAVES=3}" OUT=${OUT:-r03corun} STEPS=${STEPS:-10} TESTS= bash tools/r03_ab.sh
+AB="${AB:--;TNS_MSM_STAGGER=1;TNS_MSM_STAGGER=1 TNS_ACC_WAVES=3}" OUT=${OUT:-r03corun} STEPS=${STEPS:-10} TESTS= bash tools/ab/r03_ab.sh

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: C4 bench A/B over environment settings, alternating: tools/r04_ab_env.sh <reps> "VAR=a" "VAR=b" ...
+# round 4: C4 bench A/B over environment settings, alternating: tools/ab/r04_ab_env.sh <reps> "VAR=a" "VAR=b" ...
 set -uo pipefail
 reps=$1; shift
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 4: C4 bench + C2 MSM, default library vs one variant build (libtns_<tag>.so), alternating
-#   tools/r04_ab_lib.sh <tag> [reps]
+#   tools/ab/r04_ab_lib.sh <tag> [reps]
 set -uo pipefail
 tag=$1; reps=${2:-3}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
