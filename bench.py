@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--sumcheck-logs", default="20,24",
                     help="generic sum-check extra: degree-3 composition of three 2^k tables, for each k "
                          "(empty: skip)")
+    ap.add_argument("--tau-free-log", type=int, default=20,
+                    help="tau-less SRS extra: Lagrange basis from g1_powers alone at 2^k nodes, timed and "
+                         "checked, then Twist::prove at 2^k ops on it (0: skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="fast CPU baseline threads (0: every core the process's affinity allows)")
     ap.add_argument("--dropin-steps", type=int, default=None,
@@ -264,6 +267,7 @@ class DeviceState:
                 "host": platform.node(), "board_serial": _read(os.path.join(self.dev, "serial_number")) if self.dev
                 else None, "unique_id": _read(os.path.join(self.dev, "unique_id")) if self.dev else None,
                 "start": getattr(self, "begin", None), "end": getattr(self, "end", None),
+                "valu_clock_after_steps": getattr(self, "valu_clock", None),
                 "during": {"sclk_mhz": stat(0), "power_w": stat(1), "temp_edge_c": stat(2),
                            "sampler": "every 100 ms over the timed region"}}
 
@@ -454,6 +458,49 @@ def sumcheck_generic(ts, ctx, logs):
     return out
 
 
+def tau_free_route(ts, ctx, log_n=20, steps=5):
+    """The route an SRS WITHOUT tau ships with (src/utils.rs:61, :107 mark tau test-only): the
+    one-time Lagrange basis from g1_powers alone (tns_srs_prepare_lagrange_from_powers, tfree.hip),
+    timed at 2^log_n nodes and checked equal to the tau-derived basis, then Twist::prove of a
+    2^log_n-op trace (src/benchmarks.rs:88-99, setup_params(log_n - 2)) on that tau-less SRS, timed
+    beside the same proof on the setup SRS (identical proofs required).  The C4 basis (2^24) is the
+    same build at 16x the nodes (145 s measured): once built it is bit-identical to
+    the tau basis, so C4 proves at the headline rate on it."""
+    import dataclasses
+
+    n = 1 << log_n
+    pp, _ = ts.setup_params(log_n - 2, device=ctx.device)
+    srs = pp.commitment_params.srs
+    srs.prepare_lagrange(n)
+    want = srs.lagrange_points(n)
+    cp = ts.CommitmentParams.from_g1_limbs(srs.download(len(srs)), device=ctx.device)  # g1_powers only
+    t0 = time.perf_counter()
+    cp.srs.prepare_lagrange_from_powers(n)
+    t_basis = time.perf_counter() - t0
+    same_basis = bool(np.array_equal(cp.srs.lagrange_points(n), want))
+    del want
+    pp_free = dataclasses.replace(pp, commitment_params=cp, _raw=None)
+    addr, val, isw = ts.bench_trace(1 << (log_n - 2), n)
+    d_addr, d_val, d_isw = ts.DeviceBuffer(ctx, addr), ts.DeviceBuffer(ctx, val), ts.DeviceBuffer(ctx, isw)
+    proofs = {}
+
+    def run(p, key):
+        proofs[key] = ts.twist_prove_resident(p, d_addr, d_val, d_isw, n)
+
+    t_tau = timed_proofs(lambda: run(pp, "tau"), steps, 1)
+    t_free = timed_proofs(lambda: run(pp_free, "free"), steps, 1)
+    same_proof = bytes(proofs["tau"]) == bytes(proofs["free"])
+    return {"tau_free_basis_s_2^%d" % log_n: round(t_basis, 3),
+            "tau_free_basis_equals_tau_basis": same_basis,
+            "tau_free_twist_ops_per_sec_2^%d" % log_n: round(n / t_free, 1),
+            "tau_free_twist_ms_2^%d" % log_n: round(t_free * 1e3, 3),
+            "tau_twist_ms_2^%d" % log_n: round(t_tau * 1e3, 3),
+            "tau_free_proof_identical": bool(same_proof),
+            "tau_free_note": "SRS uploaded without tau (g1_powers only); Lagrange basis built from the powers "
+                             "(transposed remainder tree, GLV twiddles) then Twist::prove at 2^%d ops on it; "
+                             "C4's 2^24 basis is the same one-time build (145 s, DESIGN.md 2.8)" % log_n}
+
+
 def sharded_msm(ts, ctx, comm, pg, local, rank, world, reps=10):
     """C2 at N ranks: KZGCommitment::commit of 2^20 Fr::rand scalars (ChaCha20Rng([7;32]),
     setup_params(18)) sharded over the ranks (tns_msm_sharded: per-rank partial MSM over its SRS
@@ -604,6 +651,10 @@ def main():
     barrier_sync(pg, local)
     dt = time.perf_counter() - t0
     dstate.stop()
+    try:  # the clock the card holds under the accumulation's kind of load, right after the steps
+        dstate.valu_clock = ts.clock_probe(ctx, 60.0)
+    except Exception as e:  # diagnostic only
+        dstate.valu_clock = {"error": str(e)}
     if sharded:
         comm_cfg["per_rank"] = per_rank_exchange_record(pg, rank, dt, args.steps, cs0, comm.stats())
         comm_cfg["exchange_timeout_s"] = args.exchange_timeout
@@ -690,6 +741,8 @@ def main():
     if sharded and not args.no_extras:  # the MSM half of the metric at N GPUs (C2 sharded)
         with exchange_guard(ts, rank, "KZG MSM 2^20 (sharded)"):
             out.update(sharded_msm(ts, ctx, comm, pg, local, rank, world))
+    if rank == 0 and world == 1 and not args.no_extras and args.tau_free_log > 0:
+        out["tau_free_route"] = tau_free_route(ts, ctx, args.tau_free_log)
     if rank == 0 and world == 1 and not args.no_extras and args.sumcheck_logs:
         out["sumcheck_generic"] = sumcheck_generic(ts, ctx, [int(x) for x in args.sumcheck_logs.split(",")])
     if roof is not None:

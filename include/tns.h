@@ -228,7 +228,8 @@ void tns_transcript_challenge_field_element(tns_transcript *t, const uint8_t *la
 /* ---------------------------------------------------------------- sum-check (src/sumcheck.rs:56-110) */
 /* SumCheck::prove for the closure x -> sum_t coeff_t * prod_j MLE(T_{t,j})(x) over n_tables
  * MLE tables of 2^nv entries each (degree <= 3 per variable, as the reference's 4-point
- * round interpolation assumes).  rounds_out: nv x 4 Fr; challenges_out: nv Fr (nullable). */
+ * round interpolation assumes; at most 4 tables and 64 terms, terms over the same tables
+ * combine).  rounds_out: nv x 4 Fr; challenges_out: nv Fr (nullable). */
 int tns_sumcheck_prove(tns_ctx *ctx, const uint64_t *const *tables, int n_tables, unsigned nv,
                        const uint64_t claimed_sum[4], const tns_term *terms, int n_terms,
                        tns_transcript *transcript, uint64_t *rounds_out, uint64_t final_out[4],
@@ -391,6 +392,12 @@ int tns_profile_read(tns_ctx *ctx, const char *stage, double *total_ms, uint64_t
 /* out = {summed launch ms, launches, algorithmic bytes, operations (msm_accumulate: mixed
  * additions), busy ms (union of the launch intervals: stages of the two MSM lanes overlap)} */
 int tns_profile_read_ex(tns_ctx *ctx, const char *stage, double out[5]);
+/* The shader clock the device holds under a full integer-VALU load shaped like the MSM
+ * accumulation (chains of Montgomery products on every SIMD) for about `ms` milliseconds:
+ * per workgroup, delta s_memtime / delta s_memrealtime x 100 MHz (the in-kernel clock of
+ * MI355X_MICROARCH.md's DVFS notes).  out = {median MHz, min MHz, max MHz, kernel ms}.
+ * A diagnostic beside benchmark numbers (VALU-bound kernels scale with it), not proving work. */
+int tns_clock_probe(tns_ctx *ctx, double ms, double out[4]);
 
 /* ---------------------------------------------------------------- host utilities (no device) */
 /* Batch conversions between integers and Montgomery-form Fr / Fq (multi-threaded). */

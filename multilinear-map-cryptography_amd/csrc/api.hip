@@ -1744,6 +1744,78 @@ int tns_msm_sharded(tns_ctx *ctx, const tns_srs *srs, tns_comm *comm, const uint
   });
 }
 
+// ---------------------------------------------------------------- clock probe
+// Every workgroup: a chain of `iters` Montgomery products per lane (the accumulation's
+// instruction mix), bracketed by the shader-clock and constant 100 MHz counters.
+__global__ void __launch_bounds__(256) k_clock_probe(uint32_t iters, uint32_t seed, uint64_t *__restrict__ out,
+                                                     uint32_t *__restrict__ sink) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  Fq a, b;
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    a.v[l] = (seed + threadIdx.x * 0x9e3779b9u + l * 0x85ebca6bu) & (l == 7 ? 0x0fffffffu : 0xffffffffu);
+    b.v[l] = (seed * 31u + blockIdx.x + l * 0xc2b2ae35u) & (l == 7 ? 0x0fffffffu : 0xffffffffu);
+  }
+  for (uint32_t i = 0; i < iters; i++) {
+    a = mul(a, b);
+    b = mul(b, a);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (a.v[0] == 0x12345678u && b.v[1] == 0x9abcdef0u) sink[0] = a.v[2];  // keep the chain live
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = t1 - t0;
+    out[2 * blockIdx.x + 1] = r1 - r0;
+  }
+}
+
+int tns_clock_probe(tns_ctx *ctx, double ms, double out[4]) {
+  return guarded([&]() {
+    if (!ctx || !out || !(ms > 0.0)) throw Error(TNS_ERR_INVALID_PARAMETERS, "null context/output or ms <= 0");
+    CtxScope g(&ctx->c);
+    hipStream_t st = ctx->c.stream;
+    int cus = 0;
+    TNS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->c.device));
+    const unsigned nblk = (unsigned)std::max(1, cus) * 4;  // 4 waves per SIMD
+    DevBuf dout, dsink;
+    uint64_t *d = (uint64_t *)dout.ensure(sizeof(uint64_t) * 2 * nblk);
+    uint32_t *sink = (uint32_t *)dsink.ensure(sizeof(uint32_t));
+    hipEvent_t e0, e1;
+    TNS_HIP(hipEventCreate(&e0));
+    TNS_HIP(hipEventCreate(&e1));
+    auto run = [&](uint32_t iters) {
+      TNS_HIP(hipEventRecord(e0, st));
+      k_clock_probe<<<nblk, 256, 0, st>>>(iters, 0x1234567u, d, sink);
+      TNS_LAUNCH_CHECK();
+      TNS_HIP(hipEventRecord(e1, st));
+      TNS_HIP(hipEventSynchronize(e1));
+      float t = 0.f;
+      TNS_HIP(hipEventElapsedTime(&t, e0, e1));
+      return (double)t;
+    };
+    uint32_t iters = 256;
+    double t = run(iters);
+    while (t < ms / 4 && iters < (1u << 26)) {  // calibrate to about `ms`
+      iters = (uint32_t)std::min<double>((double)(1u << 26), iters * std::max(2.0, 0.5 * ms / std::max(t, 1e-3)));
+      t = run(iters);
+    }
+    if (t < ms) t = run((uint32_t)std::min<double>((double)(1u << 30), iters * ms / std::max(t, 1e-3)));
+    std::vector<uint64_t> h(2 * nblk);
+    TNS_HIP(hipMemcpy(h.data(), d, sizeof(uint64_t) * 2 * nblk, hipMemcpyDeviceToHost));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    std::vector<double> mhz;
+    for (unsigned b = 0; b < nblk; b++)
+      if (h[2 * b + 1]) mhz.push_back(100.0 * (double)h[2 * b] / (double)h[2 * b + 1]);
+    if (mhz.empty()) throw Error(TNS_ERR_DEVICE, "clock probe: no workgroup reported");
+    std::sort(mhz.begin(), mhz.end());
+    out[0] = mhz[mhz.size() / 2];
+    out[1] = mhz.front();
+    out[2] = mhz.back();
+    out[3] = t;
+    return TNS_OK;
+  });
+}
+
 // ---------------------------------------------------------------- kernel timing (HIP events)
 int tns_profile_enable(tns_ctx *ctx, int on) {
   ctx->c.prof.enabled = on != 0;

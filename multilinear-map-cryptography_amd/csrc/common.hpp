@@ -8,6 +8,7 @@
 #include <chrono>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 #include <cstdio>
 #include <functional>
 #include <map>
@@ -94,6 +95,32 @@ struct PinnedBuf {
     hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocDefault);
     if (e != hipSuccess) throw Error(TNS_ERR_OOM, std::string("hipHostMalloc failed: ") + hipGetErrorString(e));
     bytes = n ? n : 16;
+    return p;
+  }
+};
+
+// Grow-only fine-grained (coherent, device-mapped) host buffer: a kernel's last workgroup writes
+// a small result and a flag here, and the host polls the flag instead of a stream synchronize.
+struct MappedHostBuf {
+  void *p = nullptr, *dev = nullptr;
+  size_t bytes = 0;
+  MappedHostBuf() = default;
+  MappedHostBuf(const MappedHostBuf &) = delete;
+  MappedHostBuf &operator=(const MappedHostBuf &) = delete;
+  ~MappedHostBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  void *ensure(size_t n) {
+    if (n <= bytes && p) return p;
+    if (p) (void)hipHostFree(p);
+    p = dev = nullptr;
+    bytes = 0;
+    hipError_t e = hipHostMalloc(&p, n ? n : 64, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) throw Error(TNS_ERR_OOM, std::string("hipHostMalloc failed: ") + hipGetErrorString(e));
+    e = hipHostGetDevicePointer(&dev, p, 0);
+    if (e != hipSuccess) throw Error(TNS_ERR_DEVICE, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
+    std::memset(p, 0, n ? n : 64);
+    bytes = n ? n : 64;
     return p;
   }
 };
@@ -247,6 +274,9 @@ struct Ctx {
   DevBuf scratch[8];
   DevBuf sc_pong[4];    // sum-check: second fold buffer per table (the input tables stay intact)
   DevBuf sc_half[4], sc_chal, sc_out;  // the zero-closure fold chain on the side stream
+  DevBuf sc_counter;                    // sum-check round kernel: last-workgroup counter
+  MappedHostBuf sc_mapped;              // sum-check round results + flag, polled by the host
+  uint32_t sc_seq = 0;                  // the flag value of the latest round launch
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
   hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)

@@ -20,39 +20,113 @@
 namespace tns {
 
 constexpr int MAX_SC_TABLES = 4;
-constexpr int MAX_SC_TERMS = 16;
+#ifndef TNS_SC_WAVES3
+#define TNS_SC_WAVES3 4  // waves per SIMD asked of the round kernel for <= 3 tables (A/B: 3 = no spill)
+#endif
 
 struct ScTables {
   const Fr *in[MAX_SC_TABLES];
   Fr *out[MAX_SC_TABLES];
 };
-struct ScTerms {
-  Fr coeff[MAX_SC_TERMS];
-  int8_t tab[MAX_SC_TERMS][3];
-  // coefficient kinds (set by sc_terms): 0 one, 1 minus one, 2 two, 3 any -- the round kernel
-  // multiplies by a coefficient only for kind 3 (the Twist-shaped A V - O O V + 2 O: 3 products
-  // per point instead of 6)
-  int8_t kind[MAX_SC_TERMS];
-  int n;
+// ---------------------------------------------------------------- generic compositions
+// A degree <= 3 composition sum_t c_t prod_{j in t} T_j over K <= 4 tables is rewritten on the
+// host (sc_poly) in nested form
+//     f = c + sum_i T_i (c_i + sum_{j >= i} T_j (c_ij + sum_{l >= j} c_ijl T_l))
+// with the tables renumbered for the fewest products per point: the Twist-shaped
+// A V - O O V + 2 O becomes V (A - O O) + 2 O, 2 products instead of 3.  The round kernel unrolls
+// i, j, l at compile time (table values stay in registers, no run-time selects) and branches only
+// on the uniform coefficient kinds; a coefficient multiplies only when it is not 1, -1 or 2.
+constexpr int SC_SLOTS = 35;  // 1 constant + 4 linear + 10 quadratic + 20 cubic monomials
+enum : int8_t { CK_ZERO = 0, CK_ONE = 1, CK_MONE = 2, CK_TWO = 3, CK_ANY = 4 };
+struct ScPoly {
+  Fr coef[SC_SLOTS];
+  int8_t kind[SC_SLOTS];
+  int8_t has_i[MAX_SC_TABLES];                  // some monomial starts with table i
+  int8_t i_lin[MAX_SC_TABLES];                  // ... and i's inner part is more than c_i
+  int8_t has_ij[MAX_SC_TABLES][MAX_SC_TABLES];  // some monomial starts with (i, j)
+  int8_t ij_lin[MAX_SC_TABLES][MAX_SC_TABLES];  // ... and (i, j)'s inner part is more than c_ij
 };
+__host__ __device__ constexpr int sc_slot1(int i) { return 1 + i; }
+__host__ __device__ constexpr int sc_slot2(int i, int j) { return 5 + 4 * i - i * (i - 1) / 2 + (j - i); }
+__host__ __device__ constexpr int sc_slot3(int i, int j, int l) {
+  int s = 15;
+  for (int a = 0; a < 4; a++)
+    for (int b = a; b < 4; b++)
+      for (int c = b; c < 4; c++) {
+        if (a == i && b == j && c == l) return s;
+        s++;
+      }
+  return -1;
+}
 
-// the host side of ScTerms: tables checked against k, coefficient kinds classified
-static ScTerms sc_terms(const SumcheckTerm *terms, int n_terms, int k) {
-  if (n_terms > MAX_SC_TERMS) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 16 sum-check terms");
-  ScTerms st{};
-  st.n = n_terms;
-  const Fr one = Fr::one(), two = add(one, one), minus_one = neg(one);
+// The nested form of a composition for one table order perm (perm[m] = the caller's table that
+// kernel table m reads); returns its products per evaluation point.
+static int sc_poly_for(const SumcheckTerm *terms, int n_terms, int k, const int *perm, ScPoly *out) {
+  int inv[MAX_SC_TABLES] = {0, 0, 0, 0};
+  for (int m = 0; m < k; m++) inv[perm[m]] = m;
+  Fr acc[SC_SLOTS];
+  bool used[SC_SLOTS] = {};
+  for (int t = 0; t < SC_SLOTS; t++) acc[t] = Fr::zero();
   for (int t = 0; t < n_terms; t++) {
-    const Fr &c = terms[t].coeff;
-    st.coeff[t] = c;
-    st.kind[t] = c == one ? 0 : c == minus_one ? 1 : c == two ? 2 : 3;
-    for (int j = 0; j < 3; j++) {
-      const int ix = terms[t].tab[j];
-      if (ix >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
-      st.tab[t][j] = (int8_t)ix;
-    }
+    int ix[3], d = 0;
+    for (int j = 0; j < 3; j++)
+      if (terms[t].tab[j] >= 0) ix[d++] = inv[terms[t].tab[j]];
+    std::sort(ix, ix + d);
+    const int slot = d == 0 ? 0 : d == 1 ? sc_slot1(ix[0]) : d == 2 ? sc_slot2(ix[0], ix[1]) : sc_slot3(ix[0], ix[1], ix[2]);
+    acc[slot] = add(acc[slot], terms[t].coeff);
+    used[slot] = true;
   }
-  return st;
+  ScPoly q{};
+  const Fr one = Fr::one(), two = add(one, one), mone = neg(one);
+  int muls = 0;
+  for (int t = 0; t < SC_SLOTS; t++) {
+    q.coef[t] = acc[t];
+    q.kind[t] = !used[t] || acc[t] == Fr::zero() ? CK_ZERO
+                : acc[t] == one                 ? CK_ONE
+                : acc[t] == mone                ? CK_MONE
+                : acc[t] == two                 ? CK_TWO
+                                                : CK_ANY;
+  }
+  for (int i = 0; i < k; i++) {
+    for (int j = i; j < k; j++) {
+      bool lin = false;
+      for (int l = j; l < k; l++)
+        if (q.kind[sc_slot3(i, j, l)]) {
+          lin = true;
+          muls += q.kind[sc_slot3(i, j, l)] == CK_ANY;
+        }
+      q.ij_lin[i][j] = lin;
+      q.has_ij[i][j] = lin || q.kind[sc_slot2(i, j)];
+      if (lin) muls += 1;  // T_j * (c_ij + ...)
+      else if (q.kind[sc_slot2(i, j)] == CK_ANY) muls += 1;
+      q.i_lin[i] |= q.has_ij[i][j];
+    }
+    q.has_i[i] = q.i_lin[i] || q.kind[sc_slot1(i)];
+    if (q.i_lin[i]) muls += 1;  // T_i * (c_i + ...)
+    else if (q.kind[sc_slot1(i)] == CK_ANY) muls += 1;
+  }
+  if (out) *out = q;
+  return muls;
+}
+
+// The table order with the fewest products (ties: the caller's order), and its nested form.
+static ScPoly sc_poly(const SumcheckTerm *terms, int n_terms, int k, int perm[MAX_SC_TABLES]) {
+  if (n_terms > 64) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 64 sum-check terms");
+  for (int t = 0; t < n_terms; t++)
+    for (int j = 0; j < 3; j++)
+      if (terms[t].tab[j] >= k) throw Error(TNS_ERR_INVALID_PARAMETERS, "term references a missing table");
+  int p[MAX_SC_TABLES] = {0, 1, 2, 3};
+  int best = -1;
+  do {
+    const int m = sc_poly_for(terms, n_terms, k, p, nullptr);
+    if (best < 0 || m < best) {
+      best = m;
+      std::copy(p, p + MAX_SC_TABLES, perm);
+    }
+  } while (std::next_permutation(p, p + k));
+  ScPoly q;
+  sc_poly_for(terms, n_terms, k, perm, &q);
+  return q;
 }
 
 // ---------------------------------------------------------------- wave/block reductions
@@ -130,99 +204,167 @@ Fr mle_evaluate_dev(Ctx *c, const Fr *evals, unsigned nv, const Fr *point_host) 
 }
 
 // ---------------------------------------------------------------- fused sum-check round
-// FOLD:   tables in[] have 4P entries; bind r into out[] (2P entries), then sum round values.
-// !FOLD:  tables in[] have 2P entries (first round), just sum.
-// Block partial sums (4 Fr: X = 0..3) -> partials[blockIdx.x * 4 + X].
-// SKIP1: the sum at X = 1 is not formed (the host takes it as claim - g(0): from round 1 on the
-// round polynomial's g(0) + g(1) equals the previous round's g(r) identically, src/sumcheck.rs:80-84)
-template <bool FOLD, bool TERMS, bool SKIP1 = false>
-__global__ void __launch_bounds__(256) k_sc_round(ScTables t, int k, ScTerms terms, size_t P, Fr r,
-                                                  Fr *__restrict__ partials) {
-  __shared__ Fr lds[4 * 16];
-  Fr acc[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
-  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P;
-       s += (size_t)gridDim.x * blockDim.x) {
-    Fr f0[MAX_SC_TABLES], f1[MAX_SC_TABLES];
+// A fold by r: T'[s] = T[2s] + r (T[2s+1] - T[2s]) for 2P outputs (the closure-free chain's
+// single-round passes; 2P entries written, 4P read).
+__global__ void __launch_bounds__(256) k_sc_fold(ScTables t, int k, size_t P, Fr r) {
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int i = 0; i < MAX_SC_TABLES; i++) {
       if (i < k) {
-        if (FOLD) {
-          const Fr *p = t.in[i] + 4 * s;
-          Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
-          f0[i] = add(x0, mul(r, sub(x1, x0)));
-          f1[i] = add(x2, mul(r, sub(x3, x2)));
-          t.out[i][2 * s] = f0[i];
-          t.out[i][2 * s + 1] = f1[i];
-        } else {
-          f0[i] = t.in[i][2 * s];
-          f1[i] = t.in[i][2 * s + 1];
-        }
+        const Fr *p = t.in[i] + 4 * s;
+        const Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        t.out[i][2 * s] = add(x0, mul(r, sub(x1, x0)));
+        t.out[i][2 * s + 1] = add(x2, mul(r, sub(x3, x2)));
       }
-    }
-    if (TERMS) {
-      // values at X = 0,1,2,3: f0, f1, f1 + d, f1 + 2d
-      Fr d[MAX_SC_TABLES];
-#pragma unroll
-      for (int i = 0; i < MAX_SC_TABLES; i++)
-        if (i < k) d[i] = sub(f1[i], f0[i]);
-#pragma unroll  // (a runtime x put acc[] in scratch memory)
-      for (int x = 0; x < 4; x++) {
-        if (SKIP1 && x == 1) continue;
-        Fr vx[MAX_SC_TABLES];
-#pragma unroll
-        for (int i = 0; i < MAX_SC_TABLES; i++) {
-          if (i < k) {
-            if (x == 0) vx[i] = f0[i];
-            else if (x == 1) vx[i] = f1[i];
-            else if (x == 2) vx[i] = add(f1[i], d[i]);
-            else vx[i] = add(add(f1[i], d[i]), d[i]);
-          }
-        }
-        Fr sum = Fr::zero();
-        for (int tt = 0; tt < terms.n; tt++) {
-          Fr p = Fr::one();
-          bool first = true;
-#pragma unroll
-          for (int j = 0; j < 3; j++) {
-            int ix = terms.tab[tt][j];
-            if (ix >= 0) {
-              Fr v = vx[0];
-#pragma unroll
-              for (int q = 1; q < MAX_SC_TABLES; q++)
-                if (ix == q) v = vx[q];
-              p = first ? v : mul(p, v);
-              first = false;
-            }
-          }
-          const int kind = terms.kind[tt];  // (uniform: the coefficient only where it is not +-1 or 2)
-          if (kind == 1) p = neg(p);
-          else if (kind == 2) p = add(p, p);
-          else if (kind == 3) p = mul(terms.coeff[tt], p);
-          sum = add(sum, p);
-        }
-        acc[x] = add(acc[x], sum);
-      }
-    }
-  }
-  if (TERMS) {
-    block_sum_fr<4>(acc, lds);
-    if (threadIdx.x == 0) {
-#pragma unroll
-      for (int x = 0; x < 4; x++) partials[blockIdx.x * 4 + x] = acc[x];
     }
   }
 }
 
-// Sum nb blocks' 4-vectors -> out[0..3]
-__global__ void __launch_bounds__(256) k_sum_partials4(const Fr *__restrict__ partials, int nb,
-                                                       Fr *__restrict__ out) {
+__device__ __forceinline__ Fr sc_cmul(int8_t kind, const Fr &c, const Fr &v) {
+  if (kind == CK_ONE) return v;
+  if (kind == CK_MONE) return neg(v);
+  if (kind == CK_TWO) return dbl(v);
+  return mul(c, v);
+}
+
+// the composition at one point (table values v[0..K)), nested form of ScPoly; i, j, l are
+// template parameters so every table value and coefficient slot is a compile-time index
+template <int K, int I, int J, int L>
+__device__ __forceinline__ void sc_eval_l(const ScPoly &q, const Fr (&v)[K], Fr &in2) {
+  if constexpr (L < K) {
+    constexpr int s3 = sc_slot3(I, J, L);
+    if (q.kind[s3]) in2 = add(in2, sc_cmul(q.kind[s3], q.coef[s3], v[L]));
+    sc_eval_l<K, I, J, L + 1>(q, v, in2);
+  }
+}
+template <int K, int I, int J>
+__device__ __forceinline__ void sc_eval_j(const ScPoly &q, const Fr (&v)[K], Fr &inner) {
+  if constexpr (J < K) {
+    if (q.has_ij[I][J]) {
+      constexpr int s2 = sc_slot2(I, J);
+      if (!q.ij_lin[I][J]) {
+        inner = add(inner, sc_cmul(q.kind[s2], q.coef[s2], v[J]));
+      } else {
+        Fr in2 = q.coef[s2];
+        sc_eval_l<K, I, J, J>(q, v, in2);
+        inner = add(inner, mul(v[J], in2));
+      }
+    }
+    sc_eval_j<K, I, J + 1>(q, v, inner);
+  }
+}
+template <int K, int I>
+__device__ __forceinline__ void sc_eval_i(const ScPoly &q, const Fr (&v)[K], Fr &acc) {
+  if constexpr (I < K) {
+    if (q.has_i[I]) {
+      constexpr int s1 = sc_slot1(I);
+      if (!q.i_lin[I]) {
+        acc = add(acc, sc_cmul(q.kind[s1], q.coef[s1], v[I]));
+      } else {
+        Fr inner = q.coef[s1];
+        sc_eval_j<K, I, I>(q, v, inner);
+        acc = add(acc, mul(v[I], inner));
+      }
+    }
+    sc_eval_i<K, I + 1>(q, v, acc);
+  }
+}
+template <int K>
+__device__ __forceinline__ Fr sc_eval(const ScPoly &q, const Fr (&v)[K]) {
+  Fr acc = q.coef[0];  // the constant (zero when absent)
+  sc_eval_i<K, 0>(q, v, acc);
+  return acc;
+}
+
+// Where a round kernel's last workgroup leaves the round's four sums (fine-grained host memory,
+// polled by the host: no stream synchronize, no second launch).
+struct ScResult {
+  Fr sums[4];
+  uint32_t flag;
+  uint32_t pad[7];
+};
+
+// sum nb blocks' 4-vectors of partials in one block, write them and the flag to the host
+__device__ void sc_last_block_publish(const Fr *__restrict__ partials, unsigned nb, Fr *lds, unsigned *counter,
+                                      ScResult *res, uint32_t seq) {
+  Fr b[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
+  for (unsigned bb = threadIdx.x; bb < nb; bb += blockDim.x)
+#pragma unroll
+    for (int x = 0; x < 4; x++) b[x] = add(b[x], partials[4 * (size_t)bb + x]);
+  block_sum_fr<4>(b, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) res->sums[x] = b[x];
+    *counter = 0;  // ready for the next launch (stream order)
+    __threadfence_system();
+    __hip_atomic_store(&res->flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// One sum-check round of a composition over K tables.
+// FOLD:  tables in[] have 4P entries; bind r into out[] (2P entries), then sum the round values.
+// !FOLD: tables in[] have 2P entries (round 0), just sum.
+// Points X = 0, 1, 2, 3 (SKIP1: X = 1 is not formed -- from round 1 on the host takes g(1) as
+// claim - g(0), src/sumcheck.rs:80-84; the prover checks the final value against the last claim).
+// Each block's four sums go to partials[]; the last block to finish (counter) adds them up and
+// publishes them to the host with `seq` as the flag.
+template <bool FOLD, int K, bool SKIP1>
+__global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_poly(ScTables t, ScPoly q, size_t P, Fr r, Fr *__restrict__ partials,
+                                                       unsigned *counter, ScResult *res, uint32_t seq) {
   __shared__ Fr lds[4 * 16];
-  Fr acc[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
-  for (int b = threadIdx.x; b < nb; b += blockDim.x)
-    for (int x = 0; x < 4; x++) acc[x] = add(acc[x], partials[b * 4 + x]);
-  block_sum_fr<4>(acc, lds);
-  if (threadIdx.x == 0)
-    for (int x = 0; x < 4; x++) out[x] = acc[x];
+  __shared__ int last;
+  Fr acc0 = Fr::zero(), acc1 = Fr::zero(), acc2 = Fr::zero(), acc3 = Fr::zero();
+  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
+    Fr f0[K], f1[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      if (FOLD) {
+        const Fr *p = t.in[i] + 4 * s;
+        const Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        f0[i] = add(x0, mul(r, sub(x1, x0)));
+        f1[i] = add(x2, mul(r, sub(x3, x2)));
+        t.out[i][2 * s] = f0[i];
+        t.out[i][2 * s + 1] = f1[i];
+      } else {
+        f0[i] = t.in[i][2 * s];
+        f1[i] = t.in[i][2 * s + 1];
+      }
+    }
+    acc0 = add(acc0, sc_eval<K>(q, f0));
+    if (!SKIP1) acc1 = add(acc1, sc_eval<K>(q, f1));
+#pragma unroll
+    for (int i = 0; i < K; i++) f0[i] = add(f1[i], sub(f1[i], f0[i]));  // X = 2: 2 f1 - f0
+    acc2 = add(acc2, sc_eval<K>(q, f0));
+#pragma unroll
+    for (int i = 0; i < K; i++) f1[i] = add(f0[i], sub(f0[i], f1[i]));  // X = 3: 2 v2 - f1
+    acc3 = add(acc3, sc_eval<K>(q, f1));
+  }
+  Fr a[4] = {acc0, acc1, acc2, acc3};
+  block_sum_fr<4>(a, lds);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int x = 0; x < 4; x++) partials[4 * (size_t)blockIdx.x + x] = a[x];
+    __threadfence();
+    last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every block's partials (each fenced before its increment) are visible
+  sc_last_block_publish(partials, gridDim.x, lds, counter, res, seq);
+}
+
+// the last variable: table i's final value T[0] + r (T[1] - T[0]) (or T[0] when !FOLD), to the host
+__global__ void __launch_bounds__(64) k_sc_final(ScTables t, int k, Fr r, int fold, ScResult *res, uint32_t seq) {
+  if (threadIdx.x < (unsigned)k) {
+    const Fr *p = t.in[threadIdx.x];
+    res->sums[threadIdx.x] = fold ? add(p[0], mul(r, sub(p[1], p[0]))) : p[0];
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(&res->flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Closure-free sum-check (no composition terms: every round polynomial is zero, so the
@@ -255,16 +397,6 @@ __global__ void __launch_bounds__(1024) k_sc_fold_tail(ScTail t, int k, int m, c
     for (int i = 0; i < k; i++) out[i] = ((m - 1) & 1 ? t.c[i] : t.b[i])[0];
 }
 
-static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n_terms) {
-  Fr s = Fr::zero();
-  for (int t = 0; t < n_terms; t++) {
-    Fr p = terms[t].coeff;
-    for (int j = 0; j < 3; j++)
-      if (terms[t].tab[j] >= 0) p = mul(p, vals[terms[t].tab[j]]);
-    s = add(s, p);
-  }
-  return s;
-}
 
 // The zero-constraint sum-check of Twist / Shout (src/twist.rs:186-214, src/shout.rs:160-184):
 // every round polynomial is [0, 0, 0, 0], so the transcript alone yields the challenges and the
@@ -370,7 +502,7 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
     } else {
       const size_t P = n >> (rnd + 1);
       TNS_PROF_ON(c, st, "sumcheck_round", 192.0 * (double)P * k);
-      k_sc_round<true, false><<<grid_for(P, 256, 2048), 256, 0, st>>>(tt, k, ScTerms{}, P, ch[rnd - 1], nullptr);
+      k_sc_fold<<<grid_for(P, 256, 2048), 256, 0, st>>>(tt, k, P, ch[rnd - 1]);
       TNS_LAUNCH_CHECK();
       rnd += 1;
     }
@@ -396,11 +528,88 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   TNS_LAUNCH_CHECK();
 }
 
+// ---------------------------------------------------------------- generic sum-check, host side
+// Waits for a round kernel's published result: polls the flag in fine-grained host memory (the
+// last workgroup writes it); a flag that does not arrive within 30 s falls back to a stream
+// synchronize, which reports any device error, and then fails.
+static const ScResult &sc_wait(Ctx *c, uint32_t seq) {
+  volatile ScResult *res = (volatile ScResult *)c->sc_mapped.p;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 0; __atomic_load_n(&res->flag, __ATOMIC_ACQUIRE) != seq; spin++) {
+    if ((spin & 1023) == 1023 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 30.0) {
+      TNS_HIP(hipStreamSynchronize(c->stream));
+      if (__atomic_load_n(&res->flag, __ATOMIC_ACQUIRE) == seq) break;
+      throw Error(TNS_ERR_DEVICE, "sum-check round kernel did not publish its sums");
+    }
+  }
+  return *(const ScResult *)c->sc_mapped.p;
+}
+
+struct ScRun {
+  Ctx *c;
+  int k;
+  ScPoly q;
+  int perm[MAX_SC_TABLES];  // kernel table m reads the caller's table perm[m]
+  Fr *partials;
+  unsigned *counter;
+  ScResult *res_dev;
+};
+
+static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_t max_blocks) {
+  ScRun R{};
+  R.c = c;
+  R.k = k;
+  R.q = sc_poly(terms, n_terms, k, R.perm);
+  R.partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * max_blocks, 64));
+  const bool fresh = c->sc_counter.bytes == 0;
+  R.counter = (unsigned *)c->sc_counter.ensure(sizeof(unsigned));
+  if (fresh) TNS_HIP(hipMemsetAsync(R.counter, 0, sizeof(unsigned), c->stream));
+  c->sc_mapped.ensure(sizeof(ScResult));
+  R.res_dev = (ScResult *)c->sc_mapped.dev;
+  return R;
+}
+
+// one round's launch (tables already in kernel order); returns the flag value to wait for
+template <bool FOLD, bool SKIP1>
+static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P, const Fr &r) {
+  const unsigned g = grid_for(P, 256, 2048);
+  const uint32_t seq = ++R.c->sc_seq;
+  hipStream_t st = R.c->stream;
+#define TNS_SC_K(K) \
+  k_sc_round_poly<FOLD, K, SKIP1><<<g, 256, 0, st>>>(tt, R.q, P, r, R.partials, R.counter, R.res_dev, seq)
+  switch (R.k) {
+    case 1: TNS_SC_K(1); break;
+    case 2: TNS_SC_K(2); break;
+    case 3: TNS_SC_K(3); break;
+    default: TNS_SC_K(4); break;
+  }
+#undef TNS_SC_K
+  TNS_LAUNCH_CHECK();
+  return seq;
+}
+
+static void sc_round_sums(ScRun &R, uint32_t seq, Fr e[4]) {
+  const ScResult &res = sc_wait(R.c, seq);
+  for (int x = 0; x < 4; x++) e[x] = res.sums[x];
+}
+
+// the composition at one point of the caller's table order (src/sumcheck.rs:104)
+static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n_terms) {
+  Fr s = Fr::zero();
+  for (int t = 0; t < n_terms; t++) {
+    Fr p = terms[t].coeff;
+    for (int j = 0; j < 3; j++)
+      if (terms[t].tab[j] >= 0) p = mul(p, vals[terms[t].tab[j]]);
+    s = add(s, p);
+  }
+  return s;
+}
+
 // sum over {0,1}^nv of the composition (the honest prover's claimed sum): round 0's sums at
-// X = 0 and X = 1 of the fused round kernel, added
+// X = 0 and X = 1, added
 Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const SumcheckTerm *terms, int n_terms) {
   if (k < 1 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "1 to 4 sum-check tables");
-  const ScTerms st = sc_terms(terms, n_terms, k);
   if (nv == 0) {
     Fr v[MAX_SC_TABLES];
     for (int i = 0; i < k; i++) TNS_HIP(hipMemcpyAsync(&v[i], tables[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
@@ -408,18 +617,11 @@ Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Sumc
     return eval_composition_host(v, terms, n_terms);
   }
   const size_t P = (size_t)1 << (nv - 1);
-  const unsigned g = grid_for(P, 256, 2048);
-  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * (size_t)g, 64));
-  Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
+  ScRun R = sc_run(c, k, terms, n_terms, grid_for(P, 256, 2048));
   ScTables tt{};
-  for (int i = 0; i < k; i++) tt.in[i] = tables[i];
-  k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, Fr::zero(), partials);
-  TNS_LAUNCH_CHECK();
-  k_sum_partials4<<<1, 256, 0, c->stream>>>(partials, (int)g, sums_dev);
-  TNS_LAUNCH_CHECK();
+  for (int m = 0; m < k; m++) tt.in[m] = tables[R.perm[m]];
   Fr e[4];
-  TNS_HIP(hipMemcpyAsync(e, sums_dev, sizeof e, hipMemcpyDeviceToHost, c->stream));
-  TNS_HIP(hipStreamSynchronize(c->stream));
+  sc_round_sums(R, sc_launch<false, false>(R, tt, P, Fr::zero()), e);
   return add(e[0], e[1]);
 }
 
@@ -429,7 +631,6 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
                        const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                        Fr *challenges, Fr *final_vals, Fr *final_eval) {
   if (k < 0 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
-  const ScTerms st = sc_terms(terms, n_terms, k);
   const bool has_terms = n_terms > 0;
   const size_t n = (size_t)1 << nv;
   // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)); round 1
@@ -440,17 +641,14 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
     bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
     bufC[i] = (Fr *)c->sc_pong[i].ensure(sizeof(Fr) * (n / 4 + 1));
   }
-  const int nblk = (int)grid_for(n / 2 + 1, 256, 2048);
-  Fr *partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * (size_t)nblk, 64));
-  Fr *sums_dev = (Fr *)c->scratch[7].ensure(sizeof(Fr) * 4);
-
-  Fr cur = claimed;
+  ScRun R = sc_run(c, k, terms, n_terms, grid_for(n / 2 + 1, 256, 2048));
+  // kernel order m = caller's table perm[m] (the composition's cheapest nesting)
   Fr *src[MAX_SC_TABLES], *dst[MAX_SC_TABLES];
-  for (int i = 0; i < k; i++) {
-    src[i] = tables[i];
-    dst[i] = bufB[i];
+  for (int m = 0; m < k; m++) {
+    src[m] = tables[R.perm[m]];
+    dst[m] = bufB[R.perm[m]];
   }
-  Fr r_prev = Fr::zero();
+  Fr cur = claimed, r_prev = Fr::zero();
   char lab[64];
   // closure-free chains hand their last folds to k_sc_fold_tail: from round `tail_rnd` on
   // (input tables of n >> (tail_rnd - 1) <= 2^SC_TAIL_LOG entries) only the transcript runs
@@ -459,43 +657,38 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   Fr tail_ch[64];
   for (unsigned rnd = 0; rnd < nv; rnd++) {
     const size_t P = n >> (rnd + 1);  // output pairs of this round
-    const unsigned g = grid_for(P, 256, 2048);
+    Fr e[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
     if (rnd >= tail_rnd) {
       tail_ch[rnd - tail_rnd] = r_prev;  // this round's fold runs in k_sc_fold_tail
     } else {
       ScTables tt{};
-      for (int i = 0; i < k; i++) {
-        tt.in[i] = src[i];
-        tt.out[i] = dst[i];
+      for (int m = 0; m < k; m++) {
+        tt.in[m] = src[m];
+        tt.out[m] = dst[m];
       }
       TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
-      if (rnd == 0) {
-        if (has_terms) k_sc_round<false, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-      } else {
-        if (has_terms)
-          k_sc_round<true, true, true><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-        else
-          k_sc_round<true, false><<<g, 256, 0, c->stream>>>(tt, k, st, P, r_prev, partials);
-        // src now holds the freshly folded 2P-entry tables
-        for (int i = 0; i < k; i++) {
+      if (has_terms && k > 0) {
+        const uint32_t seq = rnd == 0 ? sc_launch<false, false>(R, tt, P, r_prev) : sc_launch<true, true>(R, tt, P, r_prev);
+        sc_round_sums(R, seq, e);
+      } else if (rnd > 0 && k > 0) {
+        k_sc_fold<<<grid_for(P, 256, 2048), 256, 0, c->stream>>>(tt, k, P, r_prev);
+        TNS_LAUNCH_CHECK();
+      }
+      if (has_terms && k == 0) {  // a constant composition: every point sums to c * P
+        const Fr cP = mul(eval_composition_host(nullptr, terms, n_terms), from_u64<FrCfg>((uint64_t)P));
+        for (int x = 0; x < 4; x++) e[x] = cP;
+      }
+      if (rnd > 0)  // src now holds the freshly folded 2P-entry tables
+        for (int m = 0; m < k; m++) {
           if (rnd == 1) {
-            src[i] = bufB[i];
-            dst[i] = bufC[i];
+            src[m] = bufB[R.perm[m]];
+            dst[m] = bufC[R.perm[m]];
           } else {
-            std::swap(src[i], dst[i]);
+            std::swap(src[m], dst[m]);
           }
         }
-      }
-      TNS_LAUNCH_CHECK();
     }
-    Fr e[4] = {Fr::zero(), Fr::zero(), Fr::zero(), Fr::zero()};
-    if (has_terms) {
-      k_sum_partials4<<<1, 256, 0, c->stream>>>(partials, (int)g, sums_dev);
-      TNS_LAUNCH_CHECK();
-      TNS_HIP(hipMemcpyAsync(e, sums_dev, sizeof e, hipMemcpyDeviceToHost, c->stream));
-      TNS_HIP(hipStreamSynchronize(c->stream));
-      if (rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
-    }
+    if (has_terms && rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
     Fr coeffs[4];
     interpolate4_host(e, coeffs);  // lagrange_interpolate of 4 points (src/sumcheck.rs:201-206)
     Fr g0 = horner_host(coeffs, 4, Fr::zero());
@@ -514,38 +707,43 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
     cur = horner_host(coeffs, 4, ch);
     r_prev = ch;
   }
-  // bind the last variable: final MLE values at (r_0..r_{nv-1})
+  // bind the last variable: final MLE values at (r_0..r_{nv-1}), in the caller's table order
   Fr vals[MAX_SC_TABLES];
   if (tail_rnd < nv) {
     // src: tables of n >> (tail_rnd - 1) entries; folds by the challenges of rounds
     // tail_rnd - 1 .. nv - 1 (the last one binds the final variable)
     const int m = (int)(nv - tail_rnd + 1);
     tail_ch[m - 1] = r_prev;
-    Fr *d_ch = partials, *d_out = sums_dev;
+    Fr *d_ch = R.partials, *d_out = (Fr *)c->scratch[7].ensure(sizeof(Fr) * MAX_SC_TABLES);
     TNS_HIP(hipMemcpyAsync(d_ch, tail_ch, sizeof(Fr) * m, hipMemcpyHostToDevice, c->stream));
     ScTail tl{};
-    for (int i = 0; i < k; i++) {  // src may still be the caller's table (tail from round 1)
+    for (int i = 0; i < k; i++) {  // src may still be the caller's table (tail from round 1); perm is identity here
       tl.a[i] = src[i];
       tl.b[i] = dst[i];
-      tl.c[i] = src[i] == tables[i] ? bufC[i] : src[i];
+      tl.c[i] = src[i] == tables[R.perm[i]] ? bufC[R.perm[i]] : src[i];
     }
     TNS_PROF(c, "sumcheck_round", 96.0 * (double)(n >> (tail_rnd - 1)) * k);
     k_sc_fold_tail<<<1, 1024, 0, c->stream>>>(tl, k, m, d_ch, d_out);
     TNS_LAUNCH_CHECK();
-    TNS_HIP(hipMemcpyAsync(vals, d_out, sizeof(Fr) * k, hipMemcpyDeviceToHost, c->stream));
-  } else {
-    for (int i = 0; i < k; i++) {
-      if (nv == 0) {
-        TNS_HIP(hipMemcpyAsync(&vals[i], src[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
-      } else {
-        mle_fold_dev(c, src[i], dst[i], 1, r_prev);
-        TNS_HIP(hipMemcpyAsync(&vals[i], dst[i], sizeof(Fr), hipMemcpyDeviceToHost, c->stream));
-      }
-    }
+    Fr kv[MAX_SC_TABLES];
+    TNS_HIP(hipMemcpyAsync(kv, d_out, sizeof(Fr) * k, hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipStreamSynchronize(c->stream));
+    for (int m2 = 0; m2 < k; m2++) vals[R.perm[m2]] = kv[m2];
+  } else if (k > 0) {
+    ScTables tt{};
+    for (int m2 = 0; m2 < k; m2++) tt.in[m2] = src[m2];
+    const uint32_t seq = ++c->sc_seq;
+    k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, r_prev, nv > 0, R.res_dev, seq);
+    TNS_LAUNCH_CHECK();
+    const ScResult &res = sc_wait(c, seq);
+    for (int m2 = 0; m2 < k; m2++) vals[R.perm[m2]] = res.sums[m2];
   }
-  TNS_HIP(hipStreamSynchronize(c->stream));
   for (int i = 0; i < k; i++) final_vals[i] = vals[i];
   *final_eval = eval_composition_host(vals, terms, n_terms);  // polynomial(&fixed_variables), :104
+  // the last round's claim is g_{nv-1}(r_{nv-1}) = f(r): an honest prover's final value must equal
+  // it; with g(1) taken from the claim (SKIP1) this is the check that catches a device miscompute
+  if (has_terms && nv > 0 && *final_eval != cur)
+    throw Error(TNS_ERR_SUMCHECK, "final evaluation does not match the last round's claim (device result inconsistent)");
   return TNS_OK;
 }
 

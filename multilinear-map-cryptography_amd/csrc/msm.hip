@@ -12,13 +12,15 @@
 //    reduction runs once instead of W times, no Horner doublings remain, and a wider c
 //    (fewer windows, fewer bucket additions) becomes affordable.
 //
-// Pipeline (all on one stream):
+// Pipeline (per MSM lane stream):
 //  0. k_scalar_bits: bit length of the largest scalar -> windows above it are skipped
 //     (trace commitments -- addresses, small values, flags -- are narrow).
-//  1. k_digits: scalar -> canonical -> W signed c-bit digits; key = bucket, value =
-//     point index | sign<<31; zero digits get a sentinel key.
-//  2. rocPRIM/hipCUB radix sort of the (key, value) pairs by key.
-//  3. k_bucket_bounds: [start, end) of every bucket in the sorted order.
+//  1.-3. the bucket order (bucket_sort.hip, the default): the signed c-bit digits are computed
+//     inside the first pass of a hand-written MSD counting sort (no digit array, zero digits never
+//     enter it); its last pass writes the point indices | sign<<31 alone and the bucket starts.
+//     TNS_MSM_SORT=cub (A/B) instead runs k_digits (key = bucket, sentinel for zero digits),
+//     hipCUB's radix sort of the (key, value) pairs and k_bucket_bounds -- the only use of the
+//     hipcub include below.
 //  4. k_accumulate: load-balanced -- each thread owns acc_k consecutive sorted entries
 //     and XYZZ-madds the (possibly negated) affine points run by run; runs that cross a
 //     chunk boundary leave a head/tail partial; k_bucket_fixup completes those buckets (heavy buckets'
@@ -30,7 +32,7 @@
 //     (short dependency chains -- single-thread point-add chains are the slow part).
 //  6. host: per-window Horner (per-window layout) or nothing (shared layout).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <hipcub/hipcub.hpp>  // TNS_MSM_SORT=cub only (A/B against the hand-written sort)
 
 #include <algorithm>
 #include <memory>

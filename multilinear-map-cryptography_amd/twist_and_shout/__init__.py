@@ -189,6 +189,15 @@ def device_count() -> int:
     return N.load().tns_device_count()
 
 
+def clock_probe(ctx: "Context", ms: float = 60.0) -> dict:
+    """The shader clock held under a full VALU load of Montgomery products (tns_clock_probe):
+    the in-kernel clock, median / min / max over workgroups, and the probe kernel's ms."""
+    out = (C.c_double * 4)()
+    _check(N.load().tns_clock_probe(ctx.handle, float(ms), out))
+    return {"median_mhz": round(out[0], 1), "min_mhz": round(out[1], 1), "max_mhz": round(out[2], 1),
+            "kernel_ms": round(out[3], 2)}
+
+
 def device_info(device: int = 0) -> dict:
     """hipDeviceProp_t identity and clock ratings of one visible device (tns_device_info_get)."""
     info = N.TnsDeviceInfo()

@@ -136,6 +136,7 @@ SIGNATURES = [
     ("tns_profile_enable", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_profile_only", C.c_int, [C.c_void_p, C.c_char_p]),
     ("tns_profile_read_ex", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double)]),
+    ("tns_clock_probe", C.c_int, [C.c_void_p, C.c_double, C.POINTER(C.c_double)]),
     ("tns_profile_read", C.c_int,
      [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
     ("tns_fr_rand_batch", None, [U8P, C.c_size_t, U64P]),

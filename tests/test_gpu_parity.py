@@ -350,6 +350,13 @@ COMPOSITIONS = {
     "abc": [(1, [0, 1, 2])],
     "mixed": [(3, [0, 1, 2]), (R - 5, [1]), (7, [0, 0]), (11, [])],
     "twist_like": [(1, [0, 1]), (R - 1, [2, 2, 1]), (2, [2])],
+    # every coefficient kind (1, -1, 2, general) at every nesting depth, repeated tables, terms that
+    # combine (the two [1, 2] terms) and a constant: the round kernel's nested form (sc_poly)
+    "kinds": [(1, [0]), (R - 1, [1, 2]), (2, [0, 1, 2]), (5, [2, 2]), (R - 1, [0, 0, 0]), (3, [2, 1]), (R - 2, [])],
+    # all 19 monomials of degree 1..3 over 3 tables with general coefficients (the most products)
+    "dense": [(1000003 * (i + 1) % R, ix) for i, ix in enumerate(
+        [[a] for a in range(3)] + [[a, b] for a in range(3) for b in range(a, 3)]
+        + [[a, b, c] for a in range(3) for b in range(a, 3) for c in range(b, 3)])],
 }
 
 

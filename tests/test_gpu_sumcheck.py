@@ -21,6 +21,8 @@ COMPOSITIONS = {
     "twist_like": [(1, [0, 1]), (R - 1, [2, 2, 1]), (2, [2])],
     "mixed": [(3, [0, 1, 2]), (R - 5, [1]), (7, [0, 0]), (11, [])],
     "cube4": [(5, [1, 1, 1]), (9, [3]), (1, [0, 2, 3])],
+    # four tables, general coefficients at every depth (the K = 4 round kernel's most products)
+    "dense4": [(17, [0, 1, 2]), (R - 3, [3, 3]), (5, [1, 2, 3]), (R - 1, [0]), (2, [2, 3]), (7, [])],
 }
 
 
@@ -44,7 +46,7 @@ def rand_tables(k, nv, seed):
     return out
 
 
-@pytest.mark.parametrize("nv,name", [(14, "twist_like"), (14, "mixed"), (14, "cube4"), (18, "twist_like"),
+@pytest.mark.parametrize("nv,name", [(14, "twist_like"), (14, "mixed"), (14, "cube4"), (14, "dense4"), (18, "twist_like"),
                                      (20, "twist_like"), (24, "twist_like")])
 def test_generic_sumcheck_matches_fold_oracle(nv, name):
     terms = COMPOSITIONS[name]
