@@ -94,6 +94,10 @@ def parse():
     ap.add_argument("--exchange-timeout", type=float, default=300.0,
                     help="N > 1: deadline in seconds of one exchange step of the sharded proof; a step that "
                          "misses it ends the run with exit status 3 and names the rank and step")
+    ap.add_argument("--stall-rank", type=int, default=-1,
+                    help="testing aid (N > 1): this rank sleeps --stall-s seconds before its first timed proof, "
+                         "so the others meet the exchange deadline (exit status 3)")
+    ap.add_argument("--stall-s", type=float, default=0.0)
     ap.add_argument("--rehearse-one-gpu", action="store_true",
                     help="testing aid: every rank on device 0 with a gloo process group (one-GPU box)")
     ap.add_argument("--no-msm-tables", action="store_true",
@@ -646,7 +650,9 @@ def main():
     cs0 = comm.stats() if sharded else None
     dstate.start()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for step in range(args.steps):
+        if sharded and step == 0 and rank == args.stall_rank and args.stall_s > 0:
+            time.sleep(args.stall_s)  # (--stall-rank: rehearse the exchange deadline)
         prove()
     barrier_sync(pg, local)
     dt = time.perf_counter() - t0
@@ -730,6 +736,20 @@ def main():
         t_msm = timed_proofs(lambda: ts.msm_resident(pp18.commitment_params, sc, n), 10, 1)
         out["msm_pairs_per_sec_2^20"] = round(n / t_msm, 1)
         out["msm_ms_2^20"] = round(t_msm * 1e3, 3)
+        # the same commitment with no precomputation at all (the reference's commit,
+        # src/commitments.rs:173-177, has none): variable-base Pippenger, per-window buckets
+        ref = ts.msm_resident(pp18.commitment_params, sc, n)
+        ctx.set_msm_tables(False)
+        try:
+            t_var = timed_proofs(lambda: ts.msm_resident(pp18.commitment_params, sc, n), 10, 1)
+            same = bool((ts.msm_resident(pp18.commitment_params, sc, n) == ref).all())
+        finally:
+            ctx.set_msm_tables(not args.no_msm_tables)
+        out["msm_pairs_per_sec_2^20_no_table"] = round(n / t_var, 1)
+        out["msm_ms_2^20_no_table"] = round(t_var * 1e3, 3)
+        out["msm_2^20_no_table_same_commitment"] = same
+        out["msm_2^20_table_note"] = ("msm_*_2^20: fixed-base window table over the SRS (built once at setup, "
+                                      "T[j n + i] = 2^(c j) g1_powers[i]); *_no_table: variable-base, no precomputation")
         # C3: Shout, 2^20 squares table, 2^20 lookups i % 2^20 (src/benchmarks.rs:167-177)
         T = 1 << 20
         entries = ts.fr_from_u64_array(np.arange(T, dtype=np.uint64) ** 2)

@@ -35,7 +35,10 @@ namespace tns {
 constexpr int BS_BLOCK = TNS_BS_BLOCK;  // 4 waves: fits the slots k_accumulate leaves free
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
-constexpr int BS_TILE = 8192;  // entries per tile at most (LDS staging: 64 KiB)
+#ifndef TNS_BS_TILE_MAX
+#define TNS_BS_TILE_MAX 8192
+#endif
+constexpr int BS_TILE = TNS_BS_TILE_MAX;  // entries per tile at most (LDS staging: 8 B each, 64 KiB at 8192)
 // the tile of sorts that run beside an MSM accumulation (BucketSortJob::corun): 8 entries per
 // thread, so the scatter kernels stay within the registers the accumulation leaves free
 constexpr int BS_CORUN_TILE = 2048;
@@ -776,7 +779,7 @@ static int pass_tile(int p) {
     int k = 0;
     for (const char *q = e; *q && k < 8;) {
       const int v = atoi(q);
-      t[k++] = v == 4096 ? 4096 : v == 0 ? 0 : 8192;
+      t[k++] = v == 4096 ? 4096 : v == 0 ? 0 : BS_TILE;
       while (*q && *q != ',') q++;
       if (*q == ',') q++;
     }

@@ -275,6 +275,8 @@ struct Ctx {
   DevBuf sc_pong[4];    // sum-check: second fold buffer per table (the input tables stay intact)
   DevBuf sc_half[4], sc_chal, sc_out;  // the zero-closure fold chain on the side stream
   DevBuf sc_counter;                    // sum-check round kernel: last-workgroup counter
+  DevBuf sc_poly;                       // ... and its composition (ScPoly, mle.hip)
+  PinnedBuf sc_poly_host;               // (its host staging copy)
   MappedHostBuf sc_mapped;              // sum-check round results + flag, polled by the host
   uint32_t sc_seq = 0;                  // the flag value of the latest round launch
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)

@@ -45,6 +45,7 @@ struct ScPoly {
   int8_t i_lin[MAX_SC_TABLES];                  // ... and i's inner part is more than c_i
   int8_t has_ij[MAX_SC_TABLES][MAX_SC_TABLES];  // some monomial starts with (i, j)
   int8_t ij_lin[MAX_SC_TABLES][MAX_SC_TABLES];  // ... and (i, j)'s inner part is more than c_ij
+  int8_t ij_sq[MAX_SC_TABLES][MAX_SC_TABLES];   // ... and that inner part is c_ijj T_j alone: a square
 };
 __host__ __device__ constexpr int sc_slot1(int i) { return 1 + i; }
 __host__ __device__ constexpr int sc_slot2(int i, int j) { return 5 + 4 * i - i * (i - 1) / 2 + (j - i); }
@@ -97,6 +98,9 @@ static int sc_poly_for(const SumcheckTerm *terms, int n_terms, int k, const int 
         }
       q.ij_lin[i][j] = lin;
       q.has_ij[i][j] = lin || q.kind[sc_slot2(i, j)];
+      bool only_jj = lin && !q.kind[sc_slot2(i, j)];
+      for (int l = j + 1; l < k; l++) only_jj = only_jj && !q.kind[sc_slot3(i, j, l)];
+      q.ij_sq[i][j] = only_jj;  // T_j (c_ijj T_j) = c_ijj T_j^2
       if (lin) muls += 1;  // T_j * (c_ij + ...)
       else if (q.kind[sc_slot2(i, j)] == CK_ANY) muls += 1;
       q.i_lin[i] |= q.has_ij[i][j];
@@ -220,11 +224,20 @@ __global__ void __launch_bounds__(256) k_sc_fold(ScTables t, int k, size_t P, Fr
   }
 }
 
+// The round kernel's arithmetic runs in the lazy domain [0, 2M] of the MSM accumulation
+// (bn254.hpp): products skip the final conditional subtraction (inputs <= 2M give results < 2M,
+// 4M < 2^256), sums and differences reduce against 2M; values are canonicalised only where they
+// leave the kernel (the round sums, the final table values).
+__device__ __forceinline__ Fr sc_canon(Fr a) {
+  reduce_once(a);  // [0, 2M] -> [0, M]
+  reduce_once(a);  // M -> 0
+  return a;
+}
 __device__ __forceinline__ Fr sc_cmul(int8_t kind, const Fr &c, const Fr &v) {
   if (kind == CK_ONE) return v;
-  if (kind == CK_MONE) return neg(v);
-  if (kind == CK_TWO) return dbl(v);
-  return mul(c, v);
+  if (kind == CK_MONE) return const_minus_dev<FrCfg, true>(v);  // 2M - v
+  if (kind == CK_TWO) return add2_dev(v, v);
+  return mul_lazy_dev(c, v);
 }
 
 // the composition at one point (table values v[0..K)), nested form of ScPoly; i, j, l are
@@ -233,7 +246,7 @@ template <int K, int I, int J, int L>
 __device__ __forceinline__ void sc_eval_l(const ScPoly &q, const Fr (&v)[K], Fr &in2) {
   if constexpr (L < K) {
     constexpr int s3 = sc_slot3(I, J, L);
-    if (q.kind[s3]) in2 = add(in2, sc_cmul(q.kind[s3], q.coef[s3], v[L]));
+    if (q.kind[s3]) in2 = add2_dev(in2, sc_cmul(q.kind[s3], q.coef[s3], v[L]));
     sc_eval_l<K, I, J, L + 1>(q, v, in2);
   }
 }
@@ -243,11 +256,14 @@ __device__ __forceinline__ void sc_eval_j(const ScPoly &q, const Fr (&v)[K], Fr 
     if (q.has_ij[I][J]) {
       constexpr int s2 = sc_slot2(I, J);
       if (!q.ij_lin[I][J]) {
-        inner = add(inner, sc_cmul(q.kind[s2], q.coef[s2], v[J]));
+        inner = add2_dev(inner, sc_cmul(q.kind[s2], q.coef[s2], v[J]));
+      } else if (q.ij_sq[I][J]) {  // c T_j^2: the dedicated square
+        constexpr int s3 = sc_slot3(I, J, J);
+        inner = add2_dev(inner, sc_cmul(q.kind[s3], q.coef[s3], sqr_lazy_dev(v[J])));
       } else {
         Fr in2 = q.coef[s2];
         sc_eval_l<K, I, J, J>(q, v, in2);
-        inner = add(inner, mul(v[J], in2));
+        inner = add2_dev(inner, mul_lazy_dev(v[J], in2));
       }
     }
     sc_eval_j<K, I, J + 1>(q, v, inner);
@@ -259,11 +275,11 @@ __device__ __forceinline__ void sc_eval_i(const ScPoly &q, const Fr (&v)[K], Fr 
     if (q.has_i[I]) {
       constexpr int s1 = sc_slot1(I);
       if (!q.i_lin[I]) {
-        acc = add(acc, sc_cmul(q.kind[s1], q.coef[s1], v[I]));
+        acc = add2_dev(acc, sc_cmul(q.kind[s1], q.coef[s1], v[I]));
       } else {
         Fr inner = q.coef[s1];
         sc_eval_j<K, I, I>(q, v, inner);
-        acc = add(acc, mul(v[I], inner));
+        acc = add2_dev(acc, mul_lazy_dev(v[I], inner));
       }
     }
     sc_eval_i<K, I + 1>(q, v, acc);
@@ -309,20 +325,21 @@ __device__ void sc_last_block_publish(const Fr *__restrict__ partials, unsigned 
 // Each block's four sums go to partials[]; the last block to finish (counter) adds them up and
 // publishes them to the host with `seq` as the flag.
 template <bool FOLD, int K, bool SKIP1>
-__global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_poly(ScTables t, ScPoly q, size_t P, Fr r, Fr *__restrict__ partials,
+__global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_poly(ScTables t, const ScPoly *__restrict__ qp, size_t P, Fr r, Fr *__restrict__ partials,
                                                        unsigned *counter, ScResult *res, uint32_t seq) {
   __shared__ Fr lds[4 * 16];
   __shared__ int last;
+  const ScPoly &q = *qp;  // device memory, uniform: scalar loads (a 1.2 KB kernarg spilled SGPRs)
   Fr acc0 = Fr::zero(), acc1 = Fr::zero(), acc2 = Fr::zero(), acc3 = Fr::zero();
   for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
     Fr f0[K], f1[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
-      if (FOLD) {
+      if (FOLD) {  // (lazy folds: the next round and k_sc_final read [0, 2M] values)
         const Fr *p = t.in[i] + 4 * s;
         const Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
-        f0[i] = add(x0, mul(r, sub(x1, x0)));
-        f1[i] = add(x2, mul(r, sub(x3, x2)));
+        f0[i] = add2_dev(x0, mul_lazy_dev(r, sub2_dev(x1, x0)));
+        f1[i] = add2_dev(x2, mul_lazy_dev(r, sub2_dev(x3, x2)));
         t.out[i][2 * s] = f0[i];
         t.out[i][2 * s + 1] = f1[i];
       } else {
@@ -330,16 +347,16 @@ __global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_po
         f1[i] = t.in[i][2 * s + 1];
       }
     }
-    acc0 = add(acc0, sc_eval<K>(q, f0));
-    if (!SKIP1) acc1 = add(acc1, sc_eval<K>(q, f1));
+    acc0 = add2_dev(acc0, sc_eval<K>(q, f0));
+    if (!SKIP1) acc1 = add2_dev(acc1, sc_eval<K>(q, f1));
 #pragma unroll
-    for (int i = 0; i < K; i++) f0[i] = add(f1[i], sub(f1[i], f0[i]));  // X = 2: 2 f1 - f0
-    acc2 = add(acc2, sc_eval<K>(q, f0));
+    for (int i = 0; i < K; i++) f0[i] = add2_dev(f1[i], sub2_dev(f1[i], f0[i]));  // X = 2: 2 f1 - f0
+    acc2 = add2_dev(acc2, sc_eval<K>(q, f0));
 #pragma unroll
-    for (int i = 0; i < K; i++) f1[i] = add(f0[i], sub(f0[i], f1[i]));  // X = 3: 2 v2 - f1
-    acc3 = add(acc3, sc_eval<K>(q, f1));
+    for (int i = 0; i < K; i++) f1[i] = add2_dev(f0[i], sub2_dev(f0[i], f1[i]));  // X = 3: 2 v2 - f1
+    acc3 = add2_dev(acc3, sc_eval<K>(q, f1));
   }
-  Fr a[4] = {acc0, acc1, acc2, acc3};
+  Fr a[4] = {sc_canon(acc0), sc_canon(acc1), sc_canon(acc2), sc_canon(acc3)};
   block_sum_fr<4>(a, lds);
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -357,7 +374,8 @@ __global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_po
 __global__ void __launch_bounds__(64) k_sc_final(ScTables t, int k, Fr r, int fold, ScResult *res, uint32_t seq) {
   if (threadIdx.x < (unsigned)k) {
     const Fr *p = t.in[threadIdx.x];
-    res->sums[threadIdx.x] = fold ? add(p[0], mul(r, sub(p[1], p[0]))) : p[0];
+    const Fr p0 = sc_canon(p[0]), p1 = fold ? sc_canon(p[1]) : p0;  // (lazy round-kernel folds)
+    res->sums[threadIdx.x] = fold ? add(p0, mul(r, sub(p1, p0))) : p0;
     __threadfence_system();
   }
   __syncthreads();
@@ -551,6 +569,8 @@ struct ScRun {
   int k;
   ScPoly q;
   int perm[MAX_SC_TABLES];  // kernel table m reads the caller's table perm[m]
+  const ScPoly *q_dev;
+  unsigned max_grid;
   Fr *partials;
   unsigned *counter;
   ScResult *res_dev;
@@ -561,10 +581,17 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
   R.c = c;
   R.k = k;
   R.q = sc_poly(terms, n_terms, k, R.perm);
-  R.partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * std::max<size_t>(4 * max_blocks, 64));
-  const bool fresh = c->sc_counter.bytes == 0;
+  R.max_grid = (unsigned)std::max(1, c->num_cu) * 4;  // one round of resident blocks: threads loop over s
+  ScPoly *qd = (ScPoly *)c->sc_poly.ensure(sizeof(ScPoly));
+  ScPoly *qh = (ScPoly *)c->sc_poly_host.ensure(sizeof(ScPoly));  // pinned: outlives the async copy
+  *qh = R.q;
+  TNS_HIP(hipMemcpyAsync(qd, qh, sizeof(ScPoly), hipMemcpyHostToDevice, c->stream));
+  R.q_dev = qd;
+  // (sc_launch's grids: at most max_grid * 4 one-wave blocks)
+  R.partials = (Fr *)c->scratch[6].ensure(sizeof(Fr) * 4 * std::max<size_t>(max_blocks, (size_t)R.max_grid * 4));
   R.counter = (unsigned *)c->sc_counter.ensure(sizeof(unsigned));
-  if (fresh) TNS_HIP(hipMemsetAsync(R.counter, 0, sizeof(unsigned), c->stream));
+  // zero once per sum-check (each round's last workgroup leaves it zero for the next round)
+  TNS_HIP(hipMemsetAsync(R.counter, 0, sizeof(unsigned), c->stream));
   c->sc_mapped.ensure(sizeof(ScResult));
   R.res_dev = (ScResult *)c->sc_mapped.dev;
   return R;
@@ -573,11 +600,15 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
 // one round's launch (tables already in kernel order); returns the flag value to wait for
 template <bool FOLD, bool SKIP1>
 static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P, const Fr &r) {
-  const unsigned g = grid_for(P, 256, 2048);
+  // small rounds: one-wave workgroups spread over many CUs (a round of 2^8 pairs on one 256-thread
+  // workgroup ran 35 us: one CU's multiply rate), large rounds: one round of resident 256-thread
+  // workgroups, each thread looping over pairs
+  const unsigned bs = P >= ((size_t)1 << 16) ? 256u : 64u;
+  const unsigned g = grid_for(P, bs, R.max_grid * (256 / bs));
   const uint32_t seq = ++R.c->sc_seq;
   hipStream_t st = R.c->stream;
 #define TNS_SC_K(K) \
-  k_sc_round_poly<FOLD, K, SKIP1><<<g, 256, 0, st>>>(tt, R.q, P, r, R.partials, R.counter, R.res_dev, seq)
+  k_sc_round_poly<FOLD, K, SKIP1><<<g, bs, 0, st>>>(tt, R.q_dev, P, r, R.partials, R.counter, R.res_dev, seq)
   switch (R.k) {
     case 1: TNS_SC_K(1); break;
     case 2: TNS_SC_K(2); break;
@@ -666,14 +697,17 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
         tt.in[m] = src[m];
         tt.out[m] = dst[m];
       }
-      TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
-      if (has_terms && k > 0) {
-        const uint32_t seq = rnd == 0 ? sc_launch<false, false>(R, tt, P, r_prev) : sc_launch<true, true>(R, tt, P, r_prev);
-        sc_round_sums(R, seq, e);
-      } else if (rnd > 0 && k > 0) {
-        k_sc_fold<<<grid_for(P, 256, 2048), 256, 0, c->stream>>>(tt, k, P, r_prev);
-        TNS_LAUNCH_CHECK();
+      uint32_t seq = 0;
+      {  // (the stage's HIP events bracket the launch alone, not the host's wait for its sums)
+        TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
+        if (has_terms && k > 0) {
+          seq = rnd == 0 ? sc_launch<false, false>(R, tt, P, r_prev) : sc_launch<true, true>(R, tt, P, r_prev);
+        } else if (rnd > 0 && k > 0) {
+          k_sc_fold<<<grid_for(P, 256, 2048), 256, 0, c->stream>>>(tt, k, P, r_prev);
+          TNS_LAUNCH_CHECK();
+        }
       }
+      if (seq) sc_round_sums(R, seq, e);
       if (has_terms && k == 0) {  // a constant composition: every point sums to c * P
         const Fr cP = mul(eval_composition_host(nullptr, terms, n_terms), from_u64<FrCfg>((uint64_t)P));
         for (int x = 0; x < 4; x++) e[x] = cP;
