@@ -279,6 +279,9 @@ struct Ctx {
   PinnedBuf sc_poly_host;               // (its host staging copy)
   MappedHostBuf sc_mapped;              // sum-check round results + flag, polled by the host
   uint32_t sc_seq = 0;                  // the flag value of the latest round launch
+  MappedHostBuf sc_handoff;             // sum-check challenges for pre-queued round kernels (host writes)
+  DevBuf sc_rdev;                       // ... each copied to device memory by the waiting kernel
+  uint32_t sc_chal_seq = 0;             // the flag value of the latest published challenge
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
   hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)

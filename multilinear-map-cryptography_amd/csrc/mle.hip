@@ -21,7 +21,7 @@ namespace tns {
 
 constexpr int MAX_SC_TABLES = 4;
 #ifndef TNS_SC_WAVES3
-#define TNS_SC_WAVES3 4  // waves per SIMD asked of the round kernel for <= 3 tables (A/B: 3 = no spill)
+#define TNS_SC_WAVES3 3  // waves per SIMD asked of the round kernel for <= 3 tables (4: same time, spills)
 #endif
 
 struct ScTables {
@@ -37,15 +37,18 @@ struct ScTables {
 // i, j, l at compile time (table values stay in registers, no run-time selects) and branches only
 // on the uniform coefficient kinds; a coefficient multiplies only when it is not 1, -1 or 2.
 constexpr int SC_SLOTS = 35;  // 1 constant + 4 linear + 10 quadratic + 20 cubic monomials
-enum : int8_t { CK_ZERO = 0, CK_ONE = 1, CK_MONE = 2, CK_TWO = 3, CK_ANY = 4 };
+enum : int32_t { CK_ZERO = 0, CK_ONE = 1, CK_MONE = 2, CK_TWO = 3, CK_ANY = 4 };
+// (the flags are 32-bit words: the kernel reads them with scalar loads.  As bytes they were
+// global_load_ubyte -- gfx950 has no sub-dword scalar load -- each followed by a vmcnt(0) wait
+// that also waited out the wave's table loads and fold stores: ~20 memory round trips per point)
 struct ScPoly {
   Fr coef[SC_SLOTS];
-  int8_t kind[SC_SLOTS];
-  int8_t has_i[MAX_SC_TABLES];                  // some monomial starts with table i
-  int8_t i_lin[MAX_SC_TABLES];                  // ... and i's inner part is more than c_i
-  int8_t has_ij[MAX_SC_TABLES][MAX_SC_TABLES];  // some monomial starts with (i, j)
-  int8_t ij_lin[MAX_SC_TABLES][MAX_SC_TABLES];  // ... and (i, j)'s inner part is more than c_ij
-  int8_t ij_sq[MAX_SC_TABLES][MAX_SC_TABLES];   // ... and that inner part is c_ijj T_j alone: a square
+  int32_t kind[SC_SLOTS];
+  int32_t has_i[MAX_SC_TABLES];                  // some monomial starts with table i
+  int32_t i_lin[MAX_SC_TABLES];                  // ... and i's inner part is more than c_i
+  int32_t has_ij[MAX_SC_TABLES][MAX_SC_TABLES];  // some monomial starts with (i, j)
+  int32_t ij_lin[MAX_SC_TABLES][MAX_SC_TABLES];  // ... and (i, j)'s inner part is more than c_ij
+  int32_t ij_sq[MAX_SC_TABLES][MAX_SC_TABLES];   // ... and that inner part is c_ijj T_j alone: a square
 };
 __host__ __device__ constexpr int sc_slot1(int i) { return 1 + i; }
 __host__ __device__ constexpr int sc_slot2(int i, int j) { return 5 + 4 * i - i * (i - 1) / 2 + (j - i); }
@@ -233,11 +236,13 @@ __device__ __forceinline__ Fr sc_canon(Fr a) {
   reduce_once(a);  // M -> 0
   return a;
 }
-__device__ __forceinline__ Fr sc_cmul(int8_t kind, const Fr &c, const Fr &v) {
+__device__ __forceinline__ Fr sc_mul(const Fr &a, const Fr &b) { return mul_lazy_dev(a, b); }
+__device__ __forceinline__ Fr sc_sqr(const Fr &a) { return sqr_lazy_dev(a); }
+__device__ __forceinline__ Fr sc_cmul(int32_t kind, const Fr &c, const Fr &v) {
   if (kind == CK_ONE) return v;
   if (kind == CK_MONE) return const_minus_dev<FrCfg, true>(v);  // 2M - v
   if (kind == CK_TWO) return add2_dev(v, v);
-  return mul_lazy_dev(c, v);
+  return sc_mul(c, v);
 }
 
 // the composition at one point (table values v[0..K)), nested form of ScPoly; i, j, l are
@@ -258,12 +263,12 @@ __device__ __forceinline__ void sc_eval_j(const ScPoly &q, const Fr (&v)[K], Fr 
       if (!q.ij_lin[I][J]) {
         inner = add2_dev(inner, sc_cmul(q.kind[s2], q.coef[s2], v[J]));
       } else if (q.ij_sq[I][J]) {  // c T_j^2: the dedicated square
-        constexpr int s3 = sc_slot3(I, J, J);
-        inner = add2_dev(inner, sc_cmul(q.kind[s3], q.coef[s3], sqr_lazy_dev(v[J])));
+              constexpr int s3 = sc_slot3(I, J, J);
+        inner = add2_dev(inner, sc_cmul(q.kind[s3], q.coef[s3], sc_sqr(v[J])));
       } else {
-        Fr in2 = q.coef[s2];
+              Fr in2 = q.coef[s2];
         sc_eval_l<K, I, J, J>(q, v, in2);
-        inner = add2_dev(inner, mul_lazy_dev(v[J], in2));
+        inner = add2_dev(inner, sc_mul(v[J], in2));
       }
     }
     sc_eval_j<K, I, J + 1>(q, v, inner);
@@ -277,9 +282,9 @@ __device__ __forceinline__ void sc_eval_i(const ScPoly &q, const Fr (&v)[K], Fr 
       if (!q.i_lin[I]) {
         acc = add2_dev(acc, sc_cmul(q.kind[s1], q.coef[s1], v[I]));
       } else {
-        Fr inner = q.coef[s1];
+              Fr inner = q.coef[s1];
         sc_eval_j<K, I, I>(q, v, inner);
-        acc = add2_dev(acc, mul_lazy_dev(v[I], inner));
+        acc = add2_dev(acc, sc_mul(v[I], inner));
       }
     }
     sc_eval_i<K, I + 1>(q, v, acc);
@@ -299,6 +304,43 @@ struct ScResult {
   uint32_t flag;
   uint32_t pad[7];
 };
+
+// A round's challenge handed to round kernels queued before it existed: the host writes r and then
+// the flag into ScChal (fine-grained host memory); k_sc_wait_r, queued ahead of the round kernel,
+// polls the flag and copies r into device memory (ScRDev) for the kernels behind it.  SC_CANCEL
+// (host error path) or a 5 s bound sets `abort` instead, and the kernels behind it return at once.
+struct ScChal {
+  Fr r;
+  uint32_t flag;
+  uint32_t pad[7];
+};
+struct ScRDev {
+  Fr r;
+  uint32_t abort;
+  uint32_t pad[7];
+};
+constexpr uint32_t SC_CANCEL = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(64) k_sc_wait_r(ScChal *chal, uint32_t seq, ScRDev *rd) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  uint32_t f;
+  while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) != seq && f != SC_CANCEL) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {  // 5 s: the host is gone or failed
+      f = SC_CANCEL;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  if (f == seq) {
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      rd->r.v[j] = __hip_atomic_load(&chal->r.v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    rd->abort = 0;
+  } else {
+    rd->abort = 1;
+  }
+}
 
 // sum nb blocks' 4-vectors of partials in one block, write them and the flag to the host
 __device__ void sc_last_block_publish(const Fr *__restrict__ partials, unsigned nb, Fr *lds, unsigned *counter,
@@ -322,39 +364,59 @@ __device__ void sc_last_block_publish(const Fr *__restrict__ partials, unsigned 
 // !FOLD: tables in[] have 2P entries (round 0), just sum.
 // Points X = 0, 1, 2, 3 (SKIP1: X = 1 is not formed -- from round 1 on the host takes g(1) as
 // claim - g(0), src/sumcheck.rs:80-84; the prover checks the final value against the last claim).
-// Each block's four sums go to partials[]; the last block to finish (counter) adds them up and
-// publishes them to the host with `seq` as the flag.
+// Each wave takes 64 consecutive pairs s at a time; the points are a loop over one inlined copy of
+// the composition (v walks the line f0 + X (f1 - f0)): a quarter of the code of four unrolled
+// copies, 3-4 % faster.  Each block's four sums go to partials[]; the last block to finish
+// (counter) adds them up and publishes them to the host with `seq` as the flag.
 template <bool FOLD, int K, bool SKIP1>
-__global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_poly(ScTables t, const ScPoly *__restrict__ qp, size_t P, Fr r, Fr *__restrict__ partials,
-                                                       unsigned *counter, ScResult *res, uint32_t seq) {
+__global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2)
+    k_sc_round_poly(ScTables t, const ScPoly *__restrict__ qp, size_t P, const ScRDev *rd, Fr *__restrict__ partials,
+                    unsigned *counter, ScResult *res, uint32_t seq) {
   __shared__ Fr lds[4 * 16];
   __shared__ int last;
+  if (FOLD && rd->abort) return;  // (the challenge never came: the host has given up on this proof)
+  const Fr r = FOLD ? rd->r : Fr::zero();
+  const int lane = threadIdx.x & 63;
   const ScPoly &q = *qp;  // device memory, uniform: scalar loads (a 1.2 KB kernarg spilled SGPRs)
   Fr acc0 = Fr::zero(), acc1 = Fr::zero(), acc2 = Fr::zero(), acc3 = Fr::zero();
-  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < P; s += (size_t)gridDim.x * blockDim.x) {
-    Fr f0[K], f1[K];
+  const size_t wstride = (size_t)gridDim.x * blockDim.x;
+  for (size_t base = blockIdx.x * (size_t)blockDim.x + (threadIdx.x & ~63u); base < P; base += wstride) {
+    const bool live = base + lane < P;  // (wave-uniform trip count)
+    Fr v[K], d[K];
 #pragma unroll
     for (int i = 0; i < K; i++) {
       if (FOLD) {  // (lazy folds: the next round and k_sc_final read [0, 2M] values)
-        const Fr *p = t.in[i] + 4 * s;
+        const Fr *p = t.in[i] + 4 * (base + (live ? lane : 0));
         const Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
-        f0[i] = add2_dev(x0, mul_lazy_dev(r, sub2_dev(x1, x0)));
-        f1[i] = add2_dev(x2, mul_lazy_dev(r, sub2_dev(x3, x2)));
-        t.out[i][2 * s] = f0[i];
-        t.out[i][2 * s + 1] = f1[i];
+        v[i] = add2_dev(x0, mul_lazy_dev(r, sub2_dev(x1, x0)));
+        d[i] = add2_dev(x2, mul_lazy_dev(r, sub2_dev(x3, x2)));
+        if (live) {  // (64 contiguous bytes a lane; the stores merge in L2)
+          t.out[i][2 * (base + lane)] = v[i];
+          t.out[i][2 * (base + lane) + 1] = d[i];
+        }
       } else {
-        f0[i] = t.in[i][2 * s];
-        f1[i] = t.in[i][2 * s + 1];
+        const Fr *p = t.in[i] + 2 * (base + (live ? lane : 0));
+        v[i] = p[0];
+        d[i] = p[1];
       }
+      d[i] = sub2_dev(d[i], v[i]);
     }
-    acc0 = add2_dev(acc0, sc_eval<K>(q, f0));
-    if (!SKIP1) acc1 = add2_dev(acc1, sc_eval<K>(q, f1));
+    // (every lane evaluates -- no divergent branch around the products; a lane past the last row
+    // adds zero)
+    const Fr zero = Fr::zero();
+#pragma unroll 1
+    for (int x = 0; x < 4; x++) {
+      if (!(SKIP1 && x == 1)) {
+        const Fr e = sc_eval<K>(q, v);
+        const Fr ez = live ? e : zero;
+        if (x == 0) acc0 = add2_dev(acc0, ez);
+        else if (x == 1) acc1 = add2_dev(acc1, ez);
+        else if (x == 2) acc2 = add2_dev(acc2, ez);
+        else acc3 = add2_dev(acc3, ez);
+      }
 #pragma unroll
-    for (int i = 0; i < K; i++) f0[i] = add2_dev(f1[i], sub2_dev(f1[i], f0[i]));  // X = 2: 2 f1 - f0
-    acc2 = add2_dev(acc2, sc_eval<K>(q, f0));
-#pragma unroll
-    for (int i = 0; i < K; i++) f1[i] = add2_dev(f0[i], sub2_dev(f0[i], f1[i]));  // X = 3: 2 v2 - f1
-    acc3 = add2_dev(acc3, sc_eval<K>(q, f1));
+      for (int i = 0; i < K; i++) v[i] = add2_dev(v[i], d[i]);
+    }
   }
   Fr a[4] = {sc_canon(acc0), sc_canon(acc1), sc_canon(acc2), sc_canon(acc3)};
   block_sum_fr<4>(a, lds);
@@ -370,8 +432,95 @@ __global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2) k_sc_round_po
   sc_last_block_publish(partials, gridDim.x, lds, counter, res, seq);
 }
 
+// A small round (P pairs, latency-bound: one pair's folds and points in one lane is a chain of
+// 4-12 dependent products, ~20 us at one wave per SIMD): four lanes per pair.  Lane x < K folds
+// table x's two entries, the four lanes exchange the folded values (shuffles), and lane x
+// evaluates the composition at point X = x -- a chain of 2 folds + 1 point instead of 2K folds +
+// 3-4 points.  Sums per point: lanes x, x + 4, ... of each wave, then across the grid as in
+// k_sc_round_poly (one-wave workgroups).
+template <bool FOLD, int K, bool SKIP1>
+__global__ void __launch_bounds__(64) k_sc_round_split(ScTables t, const ScPoly *__restrict__ qp, size_t P,
+                                                       const ScRDev *rd, Fr *__restrict__ partials, unsigned *counter,
+                                                       ScResult *res, uint32_t seq) {
+  __shared__ Fr lds[4 * 16];
+  __shared__ int last;
+  if (FOLD && rd->abort) return;
+  const Fr r = FOLD ? rd->r : Fr::zero();
+  const int lane = threadIdx.x, x = lane & 3;
+  const ScPoly &q = *qp;
+  const Fr zero = Fr::zero();
+  const Fr *src = t.in[0];
+  Fr *dst = t.out[0];
+#pragma unroll
+  for (int i = 1; i < K; i++)
+    if (x == i) {
+      src = t.in[i];
+      dst = t.out[i];
+    }
+  Fr acc = zero;
+  for (size_t base = (size_t)blockIdx.x * 16; base < P; base += (size_t)gridDim.x * 16) {  // (wave-uniform)
+    const size_t s = base + (lane >> 2);
+    const bool live = s < P;
+    const size_t sl = live ? s : 0;
+    Fr mv = zero, md = zero;  // this lane's table at the pair: the folded (or round-0) pair
+    if (x < K) {
+      if (FOLD) {
+        const Fr *p = src + 4 * sl;
+        const Fr x0 = p[0], x1 = p[1], x2 = p[2], x3 = p[3];
+        mv = add2_dev(x0, mul_lazy_dev(r, sub2_dev(x1, x0)));
+        md = add2_dev(x2, mul_lazy_dev(r, sub2_dev(x3, x2)));
+        if (live) {
+          dst[2 * s] = mv;
+          dst[2 * s + 1] = md;
+        }
+      } else {
+        mv = src[2 * sl];
+        md = src[2 * sl + 1];
+      }
+      md = sub2_dev(md, mv);
+    }
+    Fr w[K];
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+      const int from = (lane & ~3) | i;
+      Fr vi, di;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        vi.v[j] = __shfl(mv.v[j], from, 64);
+        di.v[j] = __shfl(md.v[j], from, 64);
+      }
+      w[i] = vi;  // the table's line at X = x: v + x d
+#pragma unroll
+      for (int j = 0; j < 3; j++)
+        if (j < x) w[i] = add2_dev(w[i], di);
+    }
+    if (!(SKIP1 && x == 1)) {
+      const Fr e = sc_eval<K>(q, w);
+      acc = add2_dev(acc, live ? e : zero);
+    }
+  }
+  acc = sc_canon(acc);
+#pragma unroll
+  for (int dd = 32; dd >= 4; dd >>= 1) {  // lanes x, x + 4, ...: lane x ends with point x's sum
+    const Fr o = shfl_down_fr(acc, dd);
+    if (lane + dd < 64) acc = add(acc, o);
+  }
+  if (lane < 4) {
+    partials[4 * (size_t)blockIdx.x + lane] = acc;
+    __threadfence();
+  }
+  __syncthreads();
+  if (lane == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // every block's partials (each fenced before its increment) are visible
+  sc_last_block_publish(partials, gridDim.x, lds, counter, res, seq);
+}
+
 // the last variable: table i's final value T[0] + r (T[1] - T[0]) (or T[0] when !FOLD), to the host
-__global__ void __launch_bounds__(64) k_sc_final(ScTables t, int k, Fr r, int fold, ScResult *res, uint32_t seq) {
+__global__ void __launch_bounds__(64) k_sc_final(ScTables t, int k, const ScRDev *rd, int fold, ScResult *res, uint32_t seq) {
+  if (fold && rd->abort) return;
+  const Fr r = fold ? rd->r : Fr::zero();
   if (threadIdx.x < (unsigned)k) {
     const Fr *p = t.in[threadIdx.x];
     const Fr p0 = sc_canon(p[0]), p1 = fold ? sc_canon(p[1]) : p0;  // (lazy round-kernel folds)
@@ -574,6 +723,9 @@ struct ScRun {
   Fr *partials;
   unsigned *counter;
   ScResult *res_dev;
+  ScChal *chal;      // host view
+  ScChal *chal_dev;  // device view
+  ScRDev *rd;
 };
 
 static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_t max_blocks) {
@@ -594,28 +746,50 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
   TNS_HIP(hipMemsetAsync(R.counter, 0, sizeof(unsigned), c->stream));
   c->sc_mapped.ensure(sizeof(ScResult));
   R.res_dev = (ScResult *)c->sc_mapped.dev;
+  R.chal = (ScChal *)c->sc_handoff.ensure(sizeof(ScChal));
+  R.chal_dev = (ScChal *)c->sc_handoff.dev;
+  R.rd = (ScRDev *)c->sc_rdev.ensure(sizeof(ScRDev));
+  TNS_HIP(hipMemsetAsync(R.rd, 0, sizeof(ScRDev), c->stream));
   return R;
 }
 
 // one round's launch (tables already in kernel order); returns the flag value to wait for
 template <bool FOLD, bool SKIP1>
-static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P, const Fr &r) {
+static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P) {
   // small rounds: one-wave workgroups spread over many CUs (a round of 2^8 pairs on one 256-thread
   // workgroup ran 35 us: one CU's multiply rate), large rounds: one round of resident 256-thread
   // workgroups, each thread looping over pairs
-  const unsigned bs = P >= ((size_t)1 << 16) ? 256u : 64u;
-  const unsigned g = grid_for(P, bs, R.max_grid * (256 / bs));
   const uint32_t seq = ++R.c->sc_seq;
   hipStream_t st = R.c->stream;
+  static const size_t split_max = [] {  // (TNS_SC_SPLIT_LOG: A/B of the split kernel's range)
+    const char *e = getenv("TNS_SC_SPLIT_LOG");
+    return e ? (size_t)1 << atoi(e) : (size_t)1 << 13;
+  }();
+  if (P <= split_max) {  // four lanes a pair, 16 pairs a one-wave block (2^12-2^14 measured alike;
+                         // at 2^16 the pairs-per-lane kernel is 2x faster)
+    const unsigned g = grid_for(P, 16, R.max_grid * 4);
 #define TNS_SC_K(K) \
-  k_sc_round_poly<FOLD, K, SKIP1><<<g, bs, 0, st>>>(tt, R.q_dev, P, r, R.partials, R.counter, R.res_dev, seq)
-  switch (R.k) {
-    case 1: TNS_SC_K(1); break;
-    case 2: TNS_SC_K(2); break;
-    case 3: TNS_SC_K(3); break;
-    default: TNS_SC_K(4); break;
-  }
+  k_sc_round_split<FOLD, K, SKIP1><<<g, 64, 0, st>>>(tt, R.q_dev, P, R.rd, R.partials, R.counter, R.res_dev, seq)
+    switch (R.k) {
+      case 1: TNS_SC_K(1); break;
+      case 2: TNS_SC_K(2); break;
+      case 3: TNS_SC_K(3); break;
+      default: TNS_SC_K(4); break;
+    }
 #undef TNS_SC_K
+  } else {
+    const unsigned bs = P >= ((size_t)1 << 16) ? 256u : 64u;
+    const unsigned g = grid_for(P, bs, R.max_grid * (256 / bs));
+#define TNS_SC_K(K) \
+  k_sc_round_poly<FOLD, K, SKIP1><<<g, bs, 0, st>>>(tt, R.q_dev, P, R.rd, R.partials, R.counter, R.res_dev, seq)
+    switch (R.k) {
+      case 1: TNS_SC_K(1); break;
+      case 2: TNS_SC_K(2); break;
+      case 3: TNS_SC_K(3); break;
+      default: TNS_SC_K(4); break;
+    }
+#undef TNS_SC_K
+  }
   TNS_LAUNCH_CHECK();
   return seq;
 }
@@ -652,8 +826,106 @@ Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Sumc
   ScTables tt{};
   for (int m = 0; m < k; m++) tt.in[m] = tables[R.perm[m]];
   Fr e[4];
-  sc_round_sums(R, sc_launch<false, false>(R, tt, P, Fr::zero()), e);
+  sc_round_sums(R, sc_launch<false, false>(R, tt, P), e);
   return add(e[0], e[1]);
+}
+
+// SumCheck::prove for a composition with terms over k >= 1 tables (sumcheck_prove_dev's main
+// case).  Round rr + 1's kernels are queued while round rr runs -- k_sc_wait_r, then the round
+// kernel -- so the host's part of a round (read the sums, interpolate, transcript, challenge) is
+// the only gap between two round kernels: the kernel launch latency (~15 us a round) leaves the
+// critical path.  TNS_SC_PREQUEUE=0 queues each round after its challenge exists (A/B).
+static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
+                                 const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
+                                 Fr *challenges, Fr *final_vals, Fr *final_eval) {
+  static const bool prequeue = [] {
+    const char *e = getenv("TNS_SC_PREQUEUE");
+    return !(e && e[0] == '0');
+  }();
+  const size_t n = (size_t)1 << nv;
+  Fr *bufB[MAX_SC_TABLES], *bufC[MAX_SC_TABLES];
+  for (int i = 0; i < k; i++) {
+    bufB[i] = (Fr *)c->scratch[2 + i].ensure(sizeof(Fr) * (n / 2 + 1));
+    bufC[i] = (Fr *)c->sc_pong[i].ensure(sizeof(Fr) * (n / 4 + 1));
+  }
+  ScRun R = sc_run(c, k, terms, n_terms, grid_for(n / 2 + 1, 256, 2048));
+  // round rr reads the caller's tables (rr <= 1) or the previous round's output and writes the
+  // folded tables into bufB (rr odd) / bufC (rr even >= 2): the caller's tables stay intact
+  auto in_of = [&](unsigned rr, int m) -> Fr * {
+    return rr <= 1 ? tables[R.perm[m]] : (rr % 2 == 0 ? bufB[R.perm[m]] : bufC[R.perm[m]]);
+  };
+  auto out_of = [&](unsigned rr, int m) -> Fr * { return rr % 2 == 1 ? bufB[R.perm[m]] : bufC[R.perm[m]]; };
+  const uint32_t chal_base = c->sc_chal_seq;
+  c->sc_chal_seq += nv + 1;
+  R.chal->flag = 0;  // (no stale value can match: chal_base + i is fresh)
+  // queue round rr (rr >= 1: behind the wait for challenge r_{rr-1}); rr == nv: the final fold
+  auto queue = [&](unsigned rr) -> uint32_t {
+    if (rr > 0) {
+      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, chal_base + rr, R.rd);
+      TNS_LAUNCH_CHECK();
+    }
+    ScTables tt{};
+    if (rr == nv) {
+      for (int m = 0; m < k; m++) tt.in[m] = nv == 1 ? tables[R.perm[m]] : out_of(nv - 1, m);
+      const uint32_t seq = ++c->sc_seq;
+      k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, R.rd, nv > 0, R.res_dev, seq);
+      TNS_LAUNCH_CHECK();
+      return seq;
+    }
+    const size_t P = n >> (rr + 1);
+    for (int m = 0; m < k; m++) {
+      tt.in[m] = in_of(rr, m);
+      tt.out[m] = out_of(rr, m);
+    }
+    TNS_PROF(c, "sumcheck_round", (rr == 0 ? 64.0 : 192.0) * (double)P * k);  // (the round kernel alone)
+    return rr == 0 ? sc_launch<false, false>(R, tt, P) : sc_launch<true, true>(R, tt, P);
+  };
+  auto publish = [&](unsigned i, const Fr &ch) {  // challenge r_i for the kernels waiting on it
+    R.chal->r = ch;
+    __atomic_store_n(&R.chal->flag, chal_base + i + 1, __ATOMIC_RELEASE);
+  };
+  try {
+    Fr cur = claimed;
+    char lab[64];
+    uint32_t seq = queue(0);  // (nv == 0: the final kernel, reading the tables as they are)
+    for (unsigned rnd = 0; rnd < nv; rnd++) {
+      const uint32_t seq_next = prequeue ? queue(rnd + 1) : 0;
+      Fr e[4];
+      sc_round_sums(R, seq, e);
+      if (rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
+      Fr coeffs[4];
+      interpolate4_host(e, coeffs);  // lagrange_interpolate of 4 points (src/sumcheck.rs:201-206)
+      if (add(horner_host(coeffs, 4, Fr::zero()), horner_host(coeffs, 4, Fr::one())) != cur) {  // :80-84
+        snprintf(lab, sizeof lab, "Round %u consistency check failed", rnd);
+        throw Error(TNS_ERR_SUMCHECK, lab);
+      }
+      for (int x = 0; x < 4; x++) rounds[4 * rnd + x] = coeffs[x];
+      snprintf(lab, sizeof lab, "sumcheck_round_%u", rnd);  // src/sumcheck.rs:90-96
+      tr.append_label(lab);
+      for (int x = 0; x < 4; x++) tr.append_fr(coeffs[x]);
+      snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
+      const Fr ch = tr.challenge(lab);
+      if (challenges) challenges[rnd] = ch;
+      cur = horner_host(coeffs, 4, ch);
+      publish(rnd, ch);
+      seq = prequeue ? seq_next : queue(rnd + 1);
+    }
+    const ScResult &res = sc_wait(c, seq);
+    Fr vals[MAX_SC_TABLES];
+    for (int m = 0; m < k; m++) vals[R.perm[m]] = res.sums[m];
+    for (int i = 0; i < k; i++) final_vals[i] = vals[i];
+    *final_eval = eval_composition_host(vals, terms, n_terms);  // polynomial(&fixed_variables), :104
+    // the last round's claim is g_{nv-1}(r_{nv-1}) = f(r): an honest prover's final value must
+    // equal it; with g(1) taken from the claim (SKIP1) this is the check that catches a device
+    // miscompute
+    if (nv > 0 && *final_eval != cur)
+      throw Error(TNS_ERR_SUMCHECK, "final evaluation does not match the last round's claim (device result inconsistent)");
+  } catch (...) {
+    // kernels may be queued behind a challenge that will never come: release them, then drain
+    __atomic_store_n(&R.chal->flag, SC_CANCEL, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(c->stream);
+    throw;
+  }
 }
 
 // SumCheck::prove (src/sumcheck.rs:56-110) for an MLE composition.
@@ -663,6 +935,10 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
                        Fr *challenges, Fr *final_vals, Fr *final_eval) {
   if (k < 0 || k > MAX_SC_TABLES) throw Error(TNS_ERR_INVALID_PARAMETERS, "at most 4 sum-check tables");
   const bool has_terms = n_terms > 0;
+  if (has_terms && k > 0) {
+    sumcheck_prove_terms(c, tables, k, nv, claimed, terms, n_terms, tr, rounds, challenges, final_vals, final_eval);
+    return TNS_OK;
+  }
   const size_t n = (size_t)1 << nv;
   // ping-pong: round r (r >= 1) reads src (2^(nv-r+1)) and writes dst (2^(nv-r)); round 1
   // reads the caller's tables, later rounds alternate between bufB and bufC, so the input
@@ -700,9 +976,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
       uint32_t seq = 0;
       {  // (the stage's HIP events bracket the launch alone, not the host's wait for its sums)
         TNS_PROF(c, "sumcheck_round", (rnd == 0 ? 64.0 : 192.0) * (double)P * k);
-        if (has_terms && k > 0) {
-          seq = rnd == 0 ? sc_launch<false, false>(R, tt, P, r_prev) : sc_launch<true, true>(R, tt, P, r_prev);
-        } else if (rnd > 0 && k > 0) {
+        if (rnd > 0 && k > 0) {  // (closure-free chain: folds only)
           k_sc_fold<<<grid_for(P, 256, 2048), 256, 0, c->stream>>>(tt, k, P, r_prev);
           TNS_LAUNCH_CHECK();
         }
@@ -767,7 +1041,13 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
     ScTables tt{};
     for (int m2 = 0; m2 < k; m2++) tt.in[m2] = src[m2];
     const uint32_t seq = ++c->sc_seq;
-    k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, r_prev, nv > 0, R.res_dev, seq);
+    if (nv > 0) {  // (the challenge to device memory: k_sc_final reads it there)
+      R.chal->r = r_prev;
+      __atomic_store_n(&R.chal->flag, ++c->sc_chal_seq, __ATOMIC_RELEASE);
+      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, c->sc_chal_seq, R.rd);
+      TNS_LAUNCH_CHECK();
+    }
+    k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, R.rd, nv > 0, R.res_dev, seq);
     TNS_LAUNCH_CHECK();
     const ScResult &res = sc_wait(c, seq);
     for (int m2 = 0; m2 < k; m2++) vals[R.perm[m2]] = res.sums[m2];

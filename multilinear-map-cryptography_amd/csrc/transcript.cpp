@@ -183,7 +183,9 @@ void interpolate4_host(const Fr e[4], Fr out[4]) {
   Fr d1 = sub(e[1], e[0]), d1b = sub(e[2], e[1]), d1c = sub(e[3], e[2]);
   Fr d2 = sub(d1b, d1), d2b = sub(d1c, d1b);
   Fr d3 = sub(d2b, d2);
-  Fr inv2 = inv(from_u64<FrCfg>(2)), inv6 = inv(from_u64<FrCfg>(6));
+  // (the two constants once: two Fermat inversions per round were ~20 us of every sum-check
+  // round's host turn)
+  static const Fr inv2 = inv(from_u64<FrCfg>(2)), inv6 = inv(from_u64<FrCfg>(6));
   Fr a0 = e[0], a1 = d1, a2 = mul(d2, inv2), a3 = mul(d3, inv6);
   // f = a0 + a1 x + a2 x(x-1) + a3 x(x-1)(x-2)
   //   = a0 + (a1 - a2 + 2 a3) x + (a2 - 3 a3) x^2 + a3 x^3

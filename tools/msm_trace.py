@@ -1,6 +1,8 @@
 """One full-width 2^k MSM over the SRS (fixed-base window tables), repeated: the sort /
 accumulate / reduction kernels without a second lane competing, for kernel traces.
-    rocprofv3 --kernel-trace --stats -d gpurun_out/msm -o run -- python3 tools/msm_trace.py 24
+    rocprofv3 --kernel-trace --stats -d gpurun_out/msm -o run -- python3 tools/msm_trace.py 24 [reps] [setup_log]
+setup_log: the SRS comes from setup_params(setup_log) (default k: 2^(k+2)+1 points); bench.py's C2
+is msm_trace.py 20 reps 18 (2^20 scalars over a 2^20+1-point SRS).
 """
 import os
 import sys
@@ -11,7 +13,8 @@ import twist_and_shout as ts  # noqa: E402
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 24
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-pp, _ = ts.setup_params(k)
+setup_log = int(sys.argv[3]) if len(sys.argv) > 3 else k
+pp, _ = ts.setup_params(setup_log)
 ctx = ts.Context.get(0)
 n = 1 << k
 sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
@@ -21,4 +24,4 @@ for _ in range(reps):
     out = ts.msm_resident(pp.commitment_params, sc, n)
     assert (out == ref).all()
 dt = (time.perf_counter() - t) / reps
-print(f"msm 2^{k}: {dt * 1e3:.3f} ms  {n / dt / 1e6:.1f} M pairs/s", flush=True)
+print(f"msm 2^{k} (setup_params({setup_log})): {dt * 1e3:.3f} ms  {n / dt / 1e6:.1f} M pairs/s", flush=True)

@@ -17,3 +17,7 @@ for k, c in agg.items():
     print(f"{k[:40]:40s} waves {c.get('SQ_WAVES',0):10.0f} valu_inst/wave {c.get('SQ_INSTS_VALU',0)/max(1,c.get('SQ_WAVES',1)):9.0f} "
           f"active_valu {c.get('SQ_ACTIVE_INST_VALU',0)/wc:5.2f} active_any {c.get('SQ_ACTIVE_INST_ANY',0)/wc:5.2f} "
           f"wait_any {c.get('SQ_WAIT_ANY',0)/wc:5.2f} wait_inst {c.get('SQ_WAIT_INST_ANY',0)/wc:5.2f}")
+    extra = {n: v for n, v in c.items() if n not in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_ANY",
+                                                     "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES")}
+    if extra:
+        print("    " + "  ".join(f"{n} {v:.4g}" for n, v in sorted(extra.items())))
