@@ -50,6 +50,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # 8 waves per SIMD, profiles/r02_macbench.txt).
 MAC_PEAK_T = 28.61
 MAC_PAIR_PEAK_T = 17.78
+MAC_PAIR_PEAK_MHZ = 2338.0  # the VALU clock macbench's pair peak was measured at (profiles/r05_macbench_clock.txt)
 # multiply-adds per lazy XYZZ mixed addition (bn254.hpp xyzz_madd_lazy): 6 products (64 + 64
 # reduction), 2 squares (36 + 64), Y3 as two products under one reduction (64 + 64 + 64)
 MACS_PER_MADD = 6 * 128 + 2 * 100 + 192
@@ -666,6 +667,15 @@ def main():
         comm_cfg["exchange_timeout_s"] = args.exchange_timeout
     breakdown = ctx.timing()
     roof, stages = roofline_from_profile(ts, ctx)
+    clk = dstate.valu_clock.get("median_mhz") if isinstance(dstate.valu_clock, dict) else None
+    if roof is not None and "compute" in roof and clk:
+        # the pair peak scales with the VALU clock (DVFS under the power cap moves it box to box by
+        # several %): the fraction at the clock this box held right after the timed steps
+        cp = roof["compute"]
+        peak_here = MAC_PAIR_PEAK_T * clk / MAC_PAIR_PEAK_MHZ
+        cp["valu_clock_mhz"] = clk
+        cp["mac_carry_pair_peak_at_clock"] = round(peak_here, 3)
+        cp["frac_of_pair_peak_at_clock"] = round(cp["achieved"] / peak_here, 4)
     stage_steps = args.steps
     if not args.profile_all_timed and args.stage_steps > 0:  # every stage, on untimed steps
         ts.profile_enable(ctx, True)
