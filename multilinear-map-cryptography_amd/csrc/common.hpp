@@ -281,6 +281,7 @@ struct Ctx {
   uint32_t sc_seq = 0;                  // the flag value of the latest round launch
   MappedHostBuf sc_handoff;             // sum-check challenges for pre-queued round kernels (host writes)
   DevBuf sc_rdev;                       // ... each copied to device memory by the waiting kernel
+  DevBuf sc_tail_sync;                  // ... and relayed between the blocks of the persistent tail
   uint32_t sc_chal_seq = 0;             // the flag value of the latest published challenge
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
   hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)

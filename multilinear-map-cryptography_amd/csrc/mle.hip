@@ -325,13 +325,16 @@ __global__ void __launch_bounds__(64) k_sc_wait_r(ScChal *chal, uint32_t seq, Sc
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   uint32_t f;
-  while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) != seq && f != SC_CANCEL) {
+  // (relaxed polls, one acquire fence after: an acquire load per poll invalidates the caches each
+  // time -- measured 2-8x slower sum-check tails with ~1000 polling blocks)
+  while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq && f != SC_CANCEL) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {  // 5 s: the host is gone or failed
       f = SC_CANCEL;
       break;
     }
     __builtin_amdgcn_s_sleep(2);
   }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   if (f == seq) {
 #pragma unroll
     for (int j = 0; j < 8; j++)
@@ -438,16 +441,12 @@ __global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2)
 // evaluates the composition at point X = x -- a chain of 2 folds + 1 point instead of 2K folds +
 // 3-4 points.  Sums per point: lanes x, x + 4, ... of each wave, then across the grid as in
 // k_sc_round_poly (one-wave workgroups).
+// one sweep of a round over pairs [0, P), 16 pairs per wave-iteration from pair 16 * blk with a
+// stride of 16 * nblk; returns lane x's sum at point x (lanes x, x + 4, ... added: lane x < 4)
 template <bool FOLD, int K, bool SKIP1>
-__global__ void __launch_bounds__(64) k_sc_round_split(ScTables t, const ScPoly *__restrict__ qp, size_t P,
-                                                       const ScRDev *rd, Fr *__restrict__ partials, unsigned *counter,
-                                                       ScResult *res, uint32_t seq) {
-  __shared__ Fr lds[4 * 16];
-  __shared__ int last;
-  if (FOLD && rd->abort) return;
-  const Fr r = FOLD ? rd->r : Fr::zero();
-  const int lane = threadIdx.x, x = lane & 3;
-  const ScPoly &q = *qp;
+__device__ __forceinline__ Fr sc_split_sweep(const ScTables &t, const ScPoly &q, size_t P, const Fr &r, size_t blk,
+                                             size_t nblk) {
+  const int lane = threadIdx.x & 63, x = lane & 3;
   const Fr zero = Fr::zero();
   const Fr *src = t.in[0];
   Fr *dst = t.out[0];
@@ -458,7 +457,7 @@ __global__ void __launch_bounds__(64) k_sc_round_split(ScTables t, const ScPoly 
       dst = t.out[i];
     }
   Fr acc = zero;
-  for (size_t base = (size_t)blockIdx.x * 16; base < P; base += (size_t)gridDim.x * 16) {  // (wave-uniform)
+  for (size_t base = blk * 16; base < P; base += nblk * 16) {  // (wave-uniform)
     const size_t s = base + (lane >> 2);
     const bool live = s < P;
     const size_t sl = live ? s : 0;
@@ -505,16 +504,140 @@ __global__ void __launch_bounds__(64) k_sc_round_split(ScTables t, const ScPoly 
     const Fr o = shfl_down_fr(acc, dd);
     if (lane + dd < 64) acc = add(acc, o);
   }
+  return acc;
+}
+
+// a one-wave block's four point sums to partials[], and the last block of the grid to finish
+// adds them up and publishes them (sc_last_block_publish)
+__device__ __forceinline__ void sc_split_finish(const Fr &acc, Fr *__restrict__ partials, unsigned *counter,
+                                                ScResult *res, uint32_t seq, Fr *lds, int *last) {
+  const int lane = threadIdx.x;
   if (lane < 4) {
     partials[4 * (size_t)blockIdx.x + lane] = acc;
     __threadfence();
   }
   __syncthreads();
-  if (lane == 0) last = atomicAdd(counter, 1u) == gridDim.x - 1;
+  if (lane == 0) *last = atomicAdd(counter, 1u) == gridDim.x - 1;
   __syncthreads();
-  if (!last) return;
+  if (!*last) return;
   __threadfence();  // every block's partials (each fenced before its increment) are visible
   sc_last_block_publish(partials, gridDim.x, lds, counter, res, seq);
+}
+
+template <bool FOLD, int K, bool SKIP1>
+__global__ void __launch_bounds__(64) k_sc_round_split(ScTables t, const ScPoly *__restrict__ qp, size_t P,
+                                                       const ScRDev *rd, Fr *__restrict__ partials, unsigned *counter,
+                                                       ScResult *res, uint32_t seq) {
+  __shared__ Fr lds[4 * 16];
+  __shared__ int last;
+  if (FOLD && rd->abort) return;
+  const Fr r = FOLD ? rd->r : Fr::zero();
+  const Fr acc = sc_split_sweep<FOLD, K, SKIP1>(t, *qp, P, r, blockIdx.x, gridDim.x);
+  sc_split_finish(acc, partials, counter, res, seq, lds, &last);
+}
+
+// The small rounds' tail in one persistent launch (rounds r0 .. nv - 1 and the final fold): a
+// round kernel per round pays two launch gaps (~5.6 us each) around the host's turn; here the
+// grid stays resident and block 0 polls the host's challenge flag, relaying each challenge to the
+// other blocks through device memory (ScTailSync: one agent-scope release per round).  The
+// round's sums leave exactly as in k_sc_round_split (last block to finish publishes to the
+// host), and the host's next challenge -- which it can only write after reading those sums --
+// orders every block's table writes of this round before any block's reads in the next.
+// Tables: round rr reads bufB (rr even) / bufC (rr odd) and writes the other; rr >= 2.
+struct ScTailSync {
+  uint32_t rflag;   // rounds whose challenge is in r[] (relayed by block 0)
+  uint32_t abort;   // block 0 saw SC_CANCEL or its 5 s bound: every block returns
+  uint32_t pad[14];
+  Fr r[64];
+};
+struct ScPing {
+  Fr *B[MAX_SC_TABLES], *C[MAX_SC_TABLES];
+};
+
+// block 0 thread 0: the host's challenge for `seq`, else false (cancel / 5 s)
+__device__ bool sc_poll_host(ScChal *chal, uint32_t seq, Fr &r) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+  uint32_t f;
+  while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq) {
+    if (f == SC_CANCEL || __builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (r itself is read with system-scope loads below)
+#pragma unroll
+  for (int j = 0; j < 8; j++) r.v[j] = __hip_atomic_load(&chal->r.v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return true;
+}
+
+template <int K>
+__global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restrict__ qp, unsigned r0, unsigned nv,
+                                                size_t n, ScChal *chal, uint32_t chal_base, ScResult *res,
+                                                uint32_t seq_base, Fr *__restrict__ partials, unsigned *counter,
+                                                ScTailSync *sync) {
+  __shared__ Fr lds[4 * 16];
+  __shared__ int last;
+  __shared__ Fr r_s;
+  __shared__ int ok_s;
+  const ScPoly &q = *qp;
+  for (unsigned rr = r0; rr <= nv; rr++) {
+    const unsigned t = rr - r0;
+    if (rr == nv && blockIdx.x != 0) return;  // (the final fold is block 0's)
+    if (threadIdx.x == 0) {  // r_{rr - 1}
+      bool ok = true;
+      Fr r;
+      if (blockIdx.x == 0) {
+        ok = sc_poll_host(chal, chal_base + rr, r);
+        if (ok) {
+          sync->r[t] = r;
+          __hip_atomic_store(&sync->rflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          __hip_atomic_store(&sync->abort, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(&sync->rflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t + 1) {
+          if (__hip_atomic_load(&sync->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ||
+              __builtin_amdgcn_s_memrealtime() - t0 > 600000000ull) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (once: the tables and r[] of this round)
+        if (ok) r = sync->r[t];
+      }
+      ok_s = ok;
+      if (ok) r_s = r;
+    }
+    __syncthreads();
+    if (!ok_s) return;
+    const Fr r = r_s;
+    ScTables tt{};
+#pragma unroll
+    for (int m = 0; m < K; m++) {  // round rr: in = bufB (rr even) / bufC (rr odd), out = the other
+      tt.in[m] = rr % 2 == 0 ? pp.B[m] : pp.C[m];
+      tt.out[m] = rr % 2 == 0 ? pp.C[m] : pp.B[m];
+    }
+    if (rr == nv) {  // the final fold: in holds the last round's 2-entry tables
+      if (blockIdx.x == 0) {
+        if (threadIdx.x < (unsigned)K) {
+          const Fr *p = tt.in[threadIdx.x];
+          const Fr p0 = sc_canon(p[0]), p1 = sc_canon(p[1]);
+          res->sums[threadIdx.x] = add(p0, mul(r, sub(p1, p0)));
+          __threadfence_system();
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          __threadfence_system();
+          __hip_atomic_store(&res->flag, seq_base + t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      return;
+    }
+    const size_t P = n >> (rr + 1);
+    const Fr acc = sc_split_sweep<true, K, true>(tt, q, P, r, blockIdx.x, gridDim.x);
+    sc_split_finish(acc, partials, counter, res, seq_base + t, lds, &last);
+    __syncthreads();  // (ok_s / r_s are rewritten by thread 0 next round)
+  }
 }
 
 // the last variable: table i's final value T[0] + r (T[1] - T[0]) (or T[0] when !FOLD), to the host
@@ -858,8 +981,52 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
   const uint32_t chal_base = c->sc_chal_seq;
   c->sc_chal_seq += nv + 1;
   R.chal->flag = 0;  // (no stale value can match: chal_base + i is fresh)
+  // the persistent tail (k_sc_tail) from the first round r0 >= 2 of <= 2^tail_log pairs
+  static const unsigned tail_log = [] {  // TNS_SC_TAIL_LOG: its range (0: no tail kernel, A/B)
+    const char *e = getenv("TNS_SC_TAIL_LOG");
+    return e ? (unsigned)atoi(e) : 13u;
+  }();
+  unsigned r0 = nv;
+  if (tail_log > 0)
+    for (unsigned rr = 2; rr < nv; rr++)
+      if ((n >> (rr + 1)) <= ((size_t)1 << tail_log)) {
+        r0 = rr;
+        break;
+      }
+  const bool tail = r0 < nv;
+  uint32_t tail_seq = 0;
   // queue round rr (rr >= 1: behind the wait for challenge r_{rr-1}); rr == nv: the final fold
   auto queue = [&](unsigned rr) -> uint32_t {
+    if (tail && rr >= r0) {  // rounds r0 .. nv - 1 and the final fold: one launch at r0
+      if (rr == r0) {
+        ScTailSync *sync = (ScTailSync *)c->sc_tail_sync.ensure(sizeof(ScTailSync));
+        TNS_HIP(hipMemsetAsync(sync, 0, sizeof(ScTailSync), c->stream));
+        ScPing pp{};
+        for (int m = 0; m < k; m++) {
+          pp.B[m] = bufB[R.perm[m]];
+          pp.C[m] = bufC[R.perm[m]];
+        }
+        tail_seq = c->sc_seq + 1;
+        c->sc_seq += nv - r0 + 1;
+        static const size_t gmax = [] {  // TNS_SC_TAIL_BLOCKS: the tail's one-wave blocks at most (A/B)
+          const char *e = getenv("TNS_SC_TAIL_BLOCKS");
+          return e ? (size_t)std::max(1, atoi(e)) : (size_t)64;  // 16 / 32 / 64 / 256 / 1024 measured
+        }();
+        const unsigned g = (unsigned)std::min<size_t>(gmax, std::max<size_t>(1, (n >> (r0 + 1)) / 16));
+#define TNS_SC_K(K)                                                                                             \
+  k_sc_tail<K><<<g, 64, 0, c->stream>>>(pp, R.q_dev, r0, nv, n, R.chal_dev, chal_base, R.res_dev, tail_seq, \
+                                       R.partials, R.counter, sync)
+        switch (k) {
+          case 1: TNS_SC_K(1); break;
+          case 2: TNS_SC_K(2); break;
+          case 3: TNS_SC_K(3); break;
+          default: TNS_SC_K(4); break;
+        }
+#undef TNS_SC_K
+        TNS_LAUNCH_CHECK();
+      }
+      return tail_seq + (rr - r0);
+    }
     if (rr > 0) {
       k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, chal_base + rr, R.rd);
       TNS_LAUNCH_CHECK();
