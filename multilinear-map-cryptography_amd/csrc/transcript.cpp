@@ -104,7 +104,9 @@ void host_fr_rand_stream(const uint8_t seed[32], size_t n, Fr *out) {
   for (size_t i = 0; i < n; i++) out[i] = fr_rand(g);
 }
 
-uint64_t siphash13_keys00(const uint8_t *m, size_t n) {
+// SipHash-1-3 with zero keys (Rust's DefaultHasher) over  prefix (8 bytes, if has_prefix) || m[0..n):
+// Hash for [u8] writes the length first, and the message is hashed in place (no concatenated copy)
+static uint64_t siphash13_keys00_pre(bool has_prefix, uint64_t prefix, const uint8_t *m, size_t n) {
   uint64_t v0 = 0x736f6d6570736575ULL, v1 = 0x646f72616e646f6dULL;
   uint64_t v2 = 0x6c7967656e657261ULL, v3 = 0x7465646279746573ULL;
   auto round = [&]() {
@@ -113,25 +115,30 @@ uint64_t siphash13_keys00(const uint8_t *m, size_t n) {
     v0 += v3; v3 = rotl64(v3, 21); v3 ^= v0;
     v2 += v1; v1 = rotl64(v1, 17); v1 ^= v2; v2 = rotl64(v2, 32);
   };
+  auto block = [&](uint64_t w) {
+    v3 ^= w;
+    round();
+    v0 ^= w;
+  };
+  if (has_prefix) block(prefix);  // (8 bytes: a whole block, the message stays block-aligned)
   size_t i = 0;
   for (; i + 8 <= n; i += 8) {
     uint64_t w;
     std::memcpy(&w, m + i, 8);  // little-endian host
-    v3 ^= w;
-    round();
-    v0 ^= w;
+    block(w);
   }
-  uint64_t b = (uint64_t)(n & 0xff) << 56;
+  const size_t total = n + (has_prefix ? 8 : 0);
+  uint64_t b = (uint64_t)(total & 0xff) << 56;
   for (size_t j = 0; i + j < n; j++) b |= (uint64_t)m[i + j] << (8 * j);
-  v3 ^= b;
-  round();
-  v0 ^= b;
+  block(b);
   v2 ^= 0xff;
   round();
   round();
   round();
   return v0 ^ v1 ^ v2 ^ v3;
 }
+
+uint64_t siphash13_keys00(const uint8_t *m, size_t n) { return siphash13_keys00_pre(false, 0, m, n); }
 
 void HostTranscript::append_label(const char *s) { append_bytes((const uint8_t *)s, std::strlen(s)); }
 void HostTranscript::append_bytes(const uint8_t *p, size_t n) { state.insert(state.end(), p, p + n); }
@@ -144,11 +151,8 @@ void HostTranscript::append_fr(const Fr &x) {
 }
 Fr HostTranscript::challenge_bytes(const uint8_t *label, size_t n) {
   append_bytes(label, n);
-  std::vector<uint8_t> msg(8 + state.size());
-  uint64_t len = state.size();
-  std::memcpy(msg.data(), &len, 8);  // Hash for [u8]: write_usize(len) first
-  if (!state.empty()) std::memcpy(msg.data() + 8, state.data(), state.size());
-  uint64_t h = siphash13_keys00(msg.data(), msg.size());
+  // Hash for [u8]: write_usize(len) first, then the bytes
+  const uint64_t h = siphash13_keys00_pre(true, (uint64_t)state.size(), state.data(), state.size());
   uint8_t seed[32];
   for (int k = 0; k < 4; k++) std::memcpy(seed + 8 * k, &h, 8);  // hash.to_le_bytes() x 4
   ChaChaStream g(seed);
