@@ -417,8 +417,10 @@ __global__ void __launch_bounds__(256, K <= 3 ? TNS_SC_WAVES3 : 2)
         else if (x == 2) acc2 = add2_dev(acc2, ez);
         else acc3 = add2_dev(acc3, ez);
       }
+      if (x < 3) {
 #pragma unroll
-      for (int i = 0; i < K; i++) v[i] = add2_dev(v[i], d[i]);
+        for (int i = 0; i < K; i++) v[i] = add2_dev(v[i], d[i]);
+      }
     }
   }
   Fr a[4] = {sc_canon(acc0), sc_canon(acc1), sc_canon(acc2), sc_canon(acc3)};
