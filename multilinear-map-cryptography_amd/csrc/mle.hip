@@ -661,9 +661,9 @@ __global__ void __launch_bounds__(64) k_sc_final(ScTables t, int k, const ScRDev
 
 // Closure-free sum-check (no composition terms: every round polynomial is zero, so the
 // challenges never wait for the device): the last m folds of the chain in one workgroup.
-// Tables of 2^m entries in a[]; fold j binds ch[j] (LSB first, as k_sc_round) and ping-pongs
+// Tables of 2^m entries in a[]; fold j binds ch[j] (LSB first, as k_sc_fold) and ping-pongs
 // a -> b -> a ...; out[i] = table i bound at all m challenges.  Replaces m - 1 small
-// k_sc_round launches and the k final k_mle_fold launches (each ~20 us of launch gap).
+// k_sc_fold launches and the k final k_mle_fold launches (each ~20 us of launch gap).
 struct ScTail {
   const Fr *a[MAX_SC_TABLES];  // first input (may be the caller's table: only read)
   Fr *b[MAX_SC_TABLES], *c[MAX_SC_TABLES];  // fold 0 -> b, then c, b, c, ...
@@ -766,7 +766,7 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   }
   Fr *d_ch = (Fr *)c->sc_chal.ensure(sizeof(Fr) * nv);
   TNS_HIP(hipMemcpyAsync(d_ch, chal_pinned, sizeof(Fr) * nv, hipMemcpyHostToDevice, st));
-  // rounds 1 .. tail_rnd - 1 fold by r_{rnd-1} in k_sc_round; the rest (tables of <= 2^12) in
+  // rounds 1 .. tail_rnd - 1 fold by r_{rnd-1} in k_sc_fold; the rest (tables of <= 2^12) in
   // one k_sc_fold_tail workgroup, down to one value per table
   const unsigned tail_rnd = sc_tail_round(nv);
   Fr *src[MAX_SC_TABLES], *dst[MAX_SC_TABLES];
