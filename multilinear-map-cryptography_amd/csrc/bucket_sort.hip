@@ -962,11 +962,17 @@ void bucket_sort_passes(BucketSortJob &J) {
     exclusive_scan(st, ln.ws[9], J.tcount, J.tbase, J.S + 1);
     if (J.last) {  // the readback; pass_rest runs after bucket_sort_finish's wait
       exclusive_scan(st, ln.ws[9], J.mcount, J.mbase, J.S + 1);
-      uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
-      TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      // the entry count (k_bs_segs1 wrote it): the accumulation sizes its chunks from it
-      TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      // (with the entry count k_bs_segs1 wrote: the accumulation sizes its chunks from it)
+      if (lane_sync_readback()) {
+        uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
+        TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      } else {
+        const void *src[3] = {J.tbase + J.S, J.mbase + J.S, J.valid};
+        const size_t by[3] = {4, 4, 4};
+        lane_publish(ln, LANE_SLOT_SORT, 3, src, by);
+      }
       J.pending = true;
       return;
     }
@@ -985,7 +991,7 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
   const uint32_t *mb = nullptr;
   size_t tiles_bound = (J.E + tile - 1) / tile + S, scan_len = (size_t)nb * tiles_bound + 1;
   if (readback) {
-    const uint32_t *h = (const uint32_t *)ln.host2.p;
+    const uint32_t *h = (const uint32_t *)J.readback;
     ident = h[1] == 0;
     tiles_bound = ident ? S : h[0];
     mb = J.mbase;
@@ -1037,10 +1043,15 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
 BucketOrder bucket_sort_finish(BucketSortJob &J) {
   MsmLane &ln = *J.ln;
   size_t entries = SIZE_MAX;  // unknown without the readback
-  if (J.pending) {
-    TNS_HIP(hipStreamSynchronize(ln.stream));  // the last pass's tile totals (host2)
+  if (J.pending) {  // the last pass's tile totals
+    if (lane_sync_readback()) {
+      TNS_HIP(hipStreamSynchronize(ln.stream));
+      J.readback = ln.host2.p;
+    } else {
+      J.readback = lane_wait(ln, LANE_SLOT_SORT);
+    }
     J.pending = false;
-    entries = ((const uint32_t *)ln.host2.p)[2];
+    entries = ((const uint32_t *)J.readback)[2];
     bucket_sort_pass_rest(J, true);
   }
   uint32_t *bstart = J.seg[J.cur];

@@ -131,9 +131,22 @@ struct MsmLane {
   hipStream_t stream = nullptr;
   DevBuf ws[18];
   DevBuf fix;       // heavy-bucket level sums
-  PinnedBuf host;   // scalar bit length, then the per-set sums
-  PinnedBuf host2;  // bucket sort: the largest last-pass segment
+  PinnedBuf host;   // scalar bit length, then the per-set sums (TNS_MSM_SYNC_READBACK=1 path)
+  PinnedBuf host2;  // bucket sort: the largest last-pass segment (TNS_MSM_SYNC_READBACK=1 path)
+  // the lane's host readbacks without a stream synchronize: a one-block kernel copies the words
+  // into this fine-grained host buffer and then sets the slot's flag, which the host polls
+  // (lane_publish / lane_wait, msm.hip).  Slots: 0 scalar bit length, 1 the sort's last-pass
+  // tile totals, 2 the MSM's per-set sums
+  MappedHostBuf mapped;
+  uint32_t pub_seq = 0;
+  uint32_t slot_seq[3] = {0, 0, 0};
 };
+// (msm.hip) readbacks through MsmLane::mapped: parts (device pointer, bytes; bytes % 4 == 0) are
+// copied back to back into the slot's data; lane_wait returns it once the flag shows the publish
+constexpr int LANE_SLOT_BITS = 0, LANE_SLOT_SORT = 1, LANE_SLOT_SUMS = 2;
+void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const size_t *bytes);
+const void *lane_wait(MsmLane &ln, int slot);
+bool lane_sync_readback();  // TNS_MSM_SYNC_READBACK=1: pinned copies + stream synchronize (A/B)
 
 // Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).
 struct InterpPlan {
@@ -553,6 +566,7 @@ struct BucketSortJob {
   int bucket_bits = 0, wb = 0, npass = 0, cur = 0, nb = 0, shift = 0, tile = 0, keybits = 0;
   int bits[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key bits per pass
   bool last = false, pending = false;
+  const void *readback = nullptr;  // the last pass's tile totals once read back (host memory)
   uint32_t *K[2] = {nullptr, nullptr}, *V[2] = {nullptr, nullptr}, *seg[2] = {nullptr, nullptr};
   uint32_t *counts = nullptr, *offs = nullptr, *tcount = nullptr, *tbase = nullptr, *desc = nullptr;
   uint32_t *mcount = nullptr, *mbase = nullptr;

@@ -35,6 +35,7 @@
 #include <hipcub/hipcub.hpp>  // TNS_MSM_SORT=cub only (A/B against the hand-written sort)
 
 #include <algorithm>
+#include <chrono>
 #include <memory>
 #include <cstdlib>
 #include <vector>
@@ -737,6 +738,72 @@ struct MsmJob {
   size_t nchunks = 0, n = 0;
 };
 
+// ---------------------------------------------------------------- lane readbacks
+struct PubArgs {
+  const uint32_t *src[4];
+  uint32_t words[4];
+  int n;
+};
+constexpr size_t LANE_MAPPED_DATA[3] = {256, 512, 1024};  // slot data offsets; flags at 64 * slot
+constexpr size_t LANE_MAPPED_BYTES = 1024 + 65536;
+
+__global__ void __launch_bounds__(256) k_lane_publish(PubArgs a, uint32_t *dst, uint32_t *flag, uint32_t seq) {
+  uint32_t off = 0;
+  for (int k = 0; k < a.n; k++) {
+    for (uint32_t i = threadIdx.x; i < a.words[k]; i += blockDim.x) dst[off + i] = a.src[k][i];
+    off += a.words[k];
+  }
+  __threadfence_system();  // every thread's words reach host memory before the flag
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+bool lane_sync_readback() {
+  static const bool v = [] {
+    const char *e = getenv("TNS_MSM_SYNC_READBACK");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const size_t *bytes) {
+  char *m = (char *)ln.mapped.ensure(LANE_MAPPED_BYTES);
+  (void)m;
+  PubArgs a{};
+  size_t total = 0;
+  a.n = n;
+  for (int k = 0; k < n; k++) {
+    a.src[k] = (const uint32_t *)src[k];
+    a.words[k] = (uint32_t)(bytes[k] / 4);
+    total += bytes[k];
+  }
+  const size_t cap = (slot == 2 ? LANE_MAPPED_BYTES : LANE_MAPPED_DATA[slot + 1]) - LANE_MAPPED_DATA[slot];
+  if (total > cap) throw Error(TNS_ERR_DEVICE, "lane readback larger than its slot");
+  const uint32_t seq = ++ln.pub_seq;
+  ln.slot_seq[slot] = seq;
+  char *dev = (char *)ln.mapped.dev;
+  k_lane_publish<<<1, 256, 0, ln.stream>>>(a, (uint32_t *)(dev + LANE_MAPPED_DATA[slot]), (uint32_t *)(dev + 64 * slot),
+                                           seq);
+  TNS_LAUNCH_CHECK();
+}
+
+const void *lane_wait(MsmLane &ln, int slot) {
+  const char *m = (const char *)ln.mapped.p;
+  const uint32_t *flag = (const uint32_t *)(m + 64 * slot), seq = ln.slot_seq[slot];
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1; __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq; spin++) {
+    if ((spin & 4095) == 0) {  // a faulted stream reports here instead of leaving the flag unset
+      const hipError_t e = hipStreamQuery(ln.stream);
+      if (e != hipSuccess && e != hipErrorNotReady) TNS_HIP(e);
+      if (e == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
+        throw Error(TNS_ERR_DEVICE, "lane readback: stream idle without its publish");
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 120.0)
+        throw Error(TNS_ERR_DEVICE, "lane readback did not arrive within 120 s");
+    }
+  }
+  return m + LANE_MAPPED_DATA[slot];
+}
+
 // the largest bit length of Montgomery scalars; the sort then reads them as they are
 // (SortInput::mont: canonicalised in its digit pass instead of through a canonical copy)
 static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
@@ -745,7 +812,13 @@ static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
   TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), ln.stream));
   k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, nullptr);
   TNS_LAUNCH_CHECK();
-  TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
+  if (lane_sync_readback()) {
+    TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
+  } else {
+    const void *src[1] = {d_bits};
+    const size_t by[1] = {sizeof(unsigned)};
+    lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
+  }
   SortInput in;
   in.fr = scalars;
   in.mont = true;
@@ -753,6 +826,7 @@ static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
 }
 
 static unsigned bits_result(MsmLane &ln) {
+  if (!lane_sync_readback()) return *(const unsigned *)lane_wait(ln, LANE_SLOT_BITS);
   TNS_HIP(hipStreamSynchronize(ln.stream));
   return *(unsigned *)ln.host.p;
 }
@@ -814,7 +888,13 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
     G1Xyzz *d = (G1Xyzz *)ln.ws[0].ensure(sizeof(G1Xyzz));
     k_msm_tiny<<<1, 64, 0, st>>>(points, scalars, (int)n, d);
     TNS_LAUNCH_CHECK();
-    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz)), d, sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+    if (lane_sync_readback()) {
+      TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz)), d, sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
+    } else {
+      const void *src[1] = {d};
+      const size_t by[1] = {sizeof(G1Xyzz)};
+      lane_publish(ln, LANE_SLOT_SUMS, 1, src, by);
+    }
     J.tiny = true;
     record_now();
     return;
@@ -1027,10 +1107,16 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
     TNS_LAUNCH_CHECK();
     sum_sets(st, parts, P.Wr * J.specs, tree ? nch / 64 : nch, tmp, out);
     const size_t fin_n = (size_t)P.Wr * J.specs;
-    char *h = (char *)ln.host.ensure(sizeof(G1Xyzz) * fin_n + 16);
-    TNS_HIP(hipMemcpyAsync(h, out, sizeof(G1Xyzz) * fin_n, hipMemcpyDeviceToHost, st));
-    // the number of sorted non-zero digits = mixed additions of k_accumulate (profiling)
-    TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    // (with the number of sorted non-zero digits = mixed additions of k_accumulate, profiling)
+    if (lane_sync_readback()) {
+      char *h = (char *)ln.host.ensure(sizeof(G1Xyzz) * fin_n + 16);
+      TNS_HIP(hipMemcpyAsync(h, out, sizeof(G1Xyzz) * fin_n, hipMemcpyDeviceToHost, st));
+      TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    } else {
+      const void *src[2] = {out, valid};
+      const size_t by[2] = {sizeof(G1Xyzz) * fin_n, sizeof(uint32_t)};
+      lane_publish(ln, LANE_SLOT_SUMS, 2, src, by);
+    }
   }
 }
 
@@ -1050,10 +1136,16 @@ static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *
 // then Horner over the windows (per-window layout).
 static G1Xyzz msm_complete(Ctx *ctx, MsmJob &J) {
   if (J.immediate) return J.result;
-  TNS_HIP(hipStreamSynchronize(J.lane->stream));
-  if (J.tiny) return *(const G1Xyzz *)J.lane->host.p;
+  const void *hp;
+  if (lane_sync_readback()) {
+    TNS_HIP(hipStreamSynchronize(J.lane->stream));
+    hp = J.lane->host.p;
+  } else {
+    hp = lane_wait(*J.lane, LANE_SLOT_SUMS);
+  }
+  if (J.tiny) return *(const G1Xyzz *)hp;
   const MsmPlan &P = J.P;
-  const G1Xyzz *fin = (const G1Xyzz *)J.lane->host.p;
+  const G1Xyzz *fin = (const G1Xyzz *)hp;
   ctx->prof.add_ops("msm_accumulate", (double)*(const uint32_t *)(fin + (size_t)P.Wr * J.specs));
   std::vector<G1Xyzz> Rw(P.Wr);
   for (int r = 0; r < P.Wr; r++) {
@@ -1110,8 +1202,14 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     if (x.prep) x.prep(ln.stream);
     if (x.n <= 64) return SortInput();
     if (!x.canon_bits) return bits_launch(ln, x.scalars, x.n);
-    TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
-                           ln.stream));
+    if (lane_sync_readback()) {
+      TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
+                             ln.stream));
+    } else {
+      const void *src[1] = {x.canon_bits};
+      const size_t by[1] = {sizeof(unsigned)};
+      lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
+    }
     SortInput in;
     if (x.u64) {
       in.u64 = x.u64;
