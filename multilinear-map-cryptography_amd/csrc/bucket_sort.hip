@@ -744,6 +744,50 @@ __global__ void __launch_bounds__(1024) k_scan_single(const uint32_t *__restrict
   }
 }
 
+// A pass's tile geometry in ONE launch (segments S + 1 <= SCAN_SMALL): tbase = exclusive scan of
+// the tiles per segment (and mbase: of the tiles of segments with >= 2 of them), computed straight
+// from the segment starts -- k_bs_tiles + one or two scans were 3-4 launches of ~5-17 us.  pub
+// (the last pass): the two totals and the entry count go to the lane's host buffer with a flag.
+__global__ void __launch_bounds__(1024) k_bs_geom(const uint32_t *__restrict__ seg, size_t S, uint32_t tile,
+                                                  uint32_t *__restrict__ tbase, uint32_t *__restrict__ mbase,
+                                                  const uint32_t *__restrict__ valid, uint32_t *pub, uint32_t *flag,
+                                                  uint32_t seq) {
+  __shared__ uint32_t lds[1024 / 64], lds2[1024 / 64];
+  const size_t n = S + 1;
+  uint32_t ct = 0, cm = 0;
+  for (size_t b0 = 0; b0 < n; b0 += (size_t)1024 * SCAN_ITEMS) {
+    const size_t base = b0 + (size_t)threadIdx.x * SCAN_ITEMS;
+    uint32_t xt[SCAN_ITEMS], xm[SCAN_ITEMS], st = 0, sm = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++) {
+      const size_t i = base + k;
+      const uint32_t t = i < S ? (seg[i + 1] - seg[i] + tile - 1) / tile : 0u;
+      xt[k] = st;
+      st += t;
+      xm[k] = sm;
+      sm += t > 1 ? t : 0u;
+    }
+    uint32_t tot_t, tot_m = 0;
+    const uint32_t off_t = ct + block_excl_scan<1024>(st, lds, tot_t);
+    const uint32_t off_m = mbase ? cm + block_excl_scan<1024>(sm, lds2, tot_m) : 0u;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS; k++)
+      if (base + k < n) {
+        tbase[base + k] = off_t + xt[k];
+        if (mbase) mbase[base + k] = off_m + xm[k];
+      }
+    ct += tot_t;
+    cm += tot_m;
+  }
+  if (pub && threadIdx.x == 0) {
+    pub[0] = ct;  // = tbase[S]
+    pub[1] = cm;  // = mbase[S]
+    pub[2] = *valid;
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // out[i] = sum_{j < i} in[j] for i < n (in and out distinct device arrays; 16-byte vector
 // loads / stores where the array is 16-byte aligned)
 static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint32_t *out, size_t n) {
@@ -956,6 +1000,29 @@ void bucket_sort_passes(BucketSortJob &J) {
     // low-magnitude buckets' segments multi-tile).  All one-tile: no geometry at all (at 2^24
     // the full layout's histograms and scan over 512 bins x every tile took 0.34 ms).
     J.last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
+    static const bool geom1 = [] {  // TNS_BS_GEOM=0: k_bs_tiles + scans (A/B)
+      const char *e = getenv("TNS_BS_GEOM");
+      return !(e && e[0] == '0');
+    }();
+    if (geom1 && J.S + 1 <= SCAN_SMALL) {
+      uint32_t *pub = nullptr, *flag = nullptr, seq = 0;
+      if (J.last && !lane_sync_readback()) lane_publish_slot(ln, LANE_SLOT_SORT, &pub, &flag, &seq);
+      k_bs_geom<<<1, 1024, 0, st>>>(seg[J.cur], J.S, (uint32_t)tile, J.tbase, J.last ? J.mbase : nullptr, J.valid,
+                                    pub, flag, seq);
+      TNS_LAUNCH_CHECK();
+      if (J.last) {
+        if (lane_sync_readback()) {
+          uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
+          TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+          TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+          TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        }
+        J.pending = true;
+        return;
+      }
+      bucket_sort_pass_rest(J, false);
+      continue;
+    }
     k_bs_tiles<<<grid_for(J.S + 1, 256), 256, 0, st>>>(seg[J.cur], J.S, (uint32_t)tile, J.tcount,
                                                          J.last ? J.mcount : nullptr);
     TNS_LAUNCH_CHECK();

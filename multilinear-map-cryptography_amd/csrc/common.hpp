@@ -146,6 +146,8 @@ struct MsmLane {
 constexpr int LANE_SLOT_BITS = 0, LANE_SLOT_SORT = 1, LANE_SLOT_SUMS = 2;
 void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const size_t *bytes);
 const void *lane_wait(MsmLane &ln, int slot);
+// for kernels that publish themselves: the slot's data and flag (device views) and its new seq
+void lane_publish_slot(MsmLane &ln, int slot, uint32_t **data, uint32_t **flag, uint32_t *seq);
 bool lane_sync_readback();  // TNS_MSM_SYNC_READBACK=1: pinned copies + stream synchronize (A/B)
 
 // Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).

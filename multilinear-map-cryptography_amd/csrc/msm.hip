@@ -787,6 +787,15 @@ void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const si
   TNS_LAUNCH_CHECK();
 }
 
+void lane_publish_slot(MsmLane &ln, int slot, uint32_t **data, uint32_t **flag, uint32_t *seq) {
+  ln.mapped.ensure(LANE_MAPPED_BYTES);
+  *seq = ++ln.pub_seq;
+  ln.slot_seq[slot] = *seq;
+  char *dev = (char *)ln.mapped.dev;
+  *data = (uint32_t *)(dev + LANE_MAPPED_DATA[slot]);
+  *flag = (uint32_t *)(dev + 64 * slot);
+}
+
 const void *lane_wait(MsmLane &ln, int slot) {
   const char *m = (const char *)ln.mapped.p;
   const uint32_t *flag = (const uint32_t *)(m + 64 * slot), seq = ln.slot_seq[slot];
