@@ -35,6 +35,10 @@ namespace tns {
 constexpr int BS_BLOCK = TNS_BS_BLOCK;  // 4 waves: fits the slots k_accumulate leaves free
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
+// the last pass may take one bit more (TNS_BS_BITS, e.g. 8,7,10: its segments stay one tile, and
+// the earlier passes get fewer bins, i.e. longer write runs): its kernels hold 1024 bins
+constexpr int BS_LASTBITS = 10;
+constexpr int BS_LASTBINS = 1 << BS_LASTBITS;
 #ifndef TNS_BS_TILE_MAX
 #define TNS_BS_TILE_MAX 8192
 #endif
@@ -140,11 +144,16 @@ __device__ __forceinline__ size_t scatter_tile() {
 #endif
 }
 
-// out[d] = sum_{d' < d} h[d'] for d < nb <= 2 * BS_BLOCK (two bins per thread)
+// out[d] = sum_{d' < d} h[d'] for d < nb <= BPT * BS_BLOCK (BPT bins per thread)
+template <int BPT = 2>
 __device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out, int nb, uint32_t *wsum) {
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const uint32_t h0 = 2 * t < nb ? h[2 * t] : 0u, h1 = 2 * t + 1 < nb ? h[2 * t + 1] : 0u;
-  const uint32_t mine = h0 + h1;
+  uint32_t hv[BPT], mine = 0;
+#pragma unroll
+  for (int q = 0; q < BPT; q++) {
+    hv[q] = BPT * t + q < nb ? h[BPT * t + q] : 0u;
+    mine += hv[q];
+  }
   uint32_t x = mine;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -155,9 +164,12 @@ __device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out
   __syncthreads();
   uint32_t off = 0;
   for (int i = 0; i < wv; i++) off += wsum[i];
-  const uint32_t ex = off + x - mine;
-  if (2 * t < nb) out[2 * t] = ex;
-  if (2 * t + 1 < nb) out[2 * t + 1] = ex + h0;
+  uint32_t ex = off + x - mine;
+#pragma unroll
+  for (int q = 0; q < BPT; q++) {
+    if (BPT * t + q < nb) out[BPT * t + q] = ex;
+    ex += hv[q];
+  }
   __syncthreads();
 }
 
@@ -443,10 +455,10 @@ __device__ __forceinline__ void tile_geom(const PassGeom &G, size_t g, uint32_t 
 
 
 // passes >= 2, histogram: counts[nbins * tbase[s] + d * T_s + k]
-template <int TILE>
+template <int TILE, int NB = BS_MAXBINS>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, size_t max_tiles,
                                                        const uint32_t *__restrict__ keys, uint32_t *__restrict__ counts) {
-  __shared__ uint32_t h[BS_MAXBINS];
+  __shared__ uint32_t h[NB];
   const size_t g = blockIdx.x;
   if (!G.mbase) {  // full layout over max_tiles slots (the compact one is sized exactly by the host)
     if (g == max_tiles - 1 && threadIdx.x == 0) counts[(size_t)G.nbins * max_tiles] = 0;
@@ -516,13 +528,13 @@ __device__ __forceinline__ uint32_t unpack_value(const PackArgs &P, uint32_t x) 
 // the scanned counts starts at offs[nbins tb]; one-tile segments (the common case in the last
 // pass) have zero counts there and take their bin offsets, and the next pass's segment
 // starts, from their own LDS scan.
-template <int TILE, int PK>
+template <int TILE, int PK, int NB = BS_MAXBINS>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, const uint32_t *__restrict__ offs,
                                                          const uint32_t *__restrict__ keys,
                                                          const uint32_t *__restrict__ vals,
                                                          uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
                                                          uint32_t *__restrict__ nseg, PackArgs P) {
-  __shared__ uint32_t h[BS_MAXBINS], lbase[BS_MAXBINS], goff[BS_MAXBINS], wsum[BS_BLOCK / 64];
+  __shared__ uint32_t h[NB], lbase[NB], goff[NB], wsum[BS_BLOCK / 64];
   constexpr int IPT = TILE / BS_BLOCK;
   __shared__ uint32_t lk[TILE], lv[PK == 2 ? 1 : TILE];
   const size_t g = scatter_tile();
@@ -558,7 +570,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
   for (int j = 0; j < IPT; j++)
     if ((int)threadIdx.x + j * BS_BLOCK < m) rk[j] = atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
   __syncthreads();
-  block_scan_bins(h, lbase, G.nbins, wsum);
+  block_scan_bins<NB / BS_BLOCK>(h, lbase, G.nbins, wsum);
   if (Ts == 1)
     for (int d = threadIdx.x; d < G.nbins; d += BS_BLOCK) {
       goff[d] = s0 + lbase[d];
@@ -899,7 +911,7 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
       if (*q == ',') q++;
     }
     bool ok = k == npass && sum == keybits;
-    for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= BS_MAXBITS;
+    for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= (p == k - 1 && k > 1 ? BS_LASTBITS : BS_MAXBITS);
     if (ok)
       for (int p = 0; p < npass; p++) bits[p] = v[p];
     if (ok)
@@ -952,7 +964,7 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   seg[1] = (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1));
   const size_t tmin = J.corun ? BS_CORUN_TILE : 4096;  // the smallest pass tile
   const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> bits[npass - 1]) + 1;
-  const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
+  const size_t cnt_len = std::max((size_t)nb * T1, (size_t)(1u << bits[npass - 1] > BS_MAXBINS ? BS_LASTBINS : BS_MAXBINS) * max_tiles) + 1;
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
@@ -993,6 +1005,7 @@ void bucket_sort_passes(BucketSortJob &J) {
     J.shift -= bits[p];
     int tile = J.corun ? BS_CORUN_TILE : pass_tile(p);
     if (!tile) tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
+    if (bits[p] > BS_MAXBITS) tile = BS_TILE;  // (the 1024-bin kernels: 8192-entry tiles only)
     J.tile = tile;
     // In the last pass most segments fit one tile and rank locally; only segments of >= 2
     // tiles need the histogram pass and the global scan, so their counts get a compact layout,
@@ -1077,7 +1090,9 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
   uint32_t *counts = J.counts, *offs = J.offs;
   if (!ident) {
     if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
-    if (tile == BS_CORUN_TILE)
+    if (nb > BS_MAXBINS)  // (a 10-bit last pass: 8192-entry tiles, 1024 bins)
+      k_bs_count<BS_TILE, BS_LASTBINS><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    else if (tile == BS_CORUN_TILE)
       k_bs_count<BS_CORUN_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     else if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
@@ -1085,7 +1100,11 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
     exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
   }
   {
-    auto *kern = tile == BS_CORUN_TILE ? (pk == 0   ? k_bs_scatter<BS_CORUN_TILE, 0>
+    auto *kern = nb > BS_MAXBINS ? (pk == 0   ? k_bs_scatter<BS_TILE, 0, BS_LASTBINS>
+                                    : pk == 1 ? k_bs_scatter<BS_TILE, 1, BS_LASTBINS>
+                                    : pk == 2 ? k_bs_scatter<BS_TILE, 2, BS_LASTBINS>
+                                              : k_bs_scatter<BS_TILE, 3, BS_LASTBINS>)
+               : tile == BS_CORUN_TILE ? (pk == 0   ? k_bs_scatter<BS_CORUN_TILE, 0>
                                           : pk == 1 ? k_bs_scatter<BS_CORUN_TILE, 1>
                                           : pk == 2 ? k_bs_scatter<BS_CORUN_TILE, 2>
                                                     : k_bs_scatter<BS_CORUN_TILE, 3>)
