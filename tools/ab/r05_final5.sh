@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5 re-validation after the bucket-sort template change: GPU suite, smoke, the bench as the driver runs it
+set -uo pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/r05_final5
+mkdir -p $out
+timeout -k 10 1500 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $out/pytest_gpu.txt 2>&1 || { tail -30 $out/pytest_gpu.txt; exit 1; }
+tail -2 $out/pytest_gpu.txt
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.txt 2>&1 || { tail -20 $out/smoke.txt; exit 1; }
+tail -1 $out/smoke.txt
+timeout -k 10 900 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.jsonl 2> $out/bench.err || { tail -20 $out/bench.err; exit 1; }
+tail -n 1 $out/bench.jsonl | cut -c1-200
