@@ -32,13 +32,25 @@ def test_chacha20_rfc8439_block():
     assert out[:4] == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3]
 
 
+# SipHash-2-4 reference-implementation vectors (key 00..0f, message 00..(n-1)), n = 0..15: every
+# tail length of the last block, one- and two-block messages -- the block loop, tail packing and
+# finalisation that SipHash-1-3 shares, pinned independently of the round counts
+SIPHASH24_VECTORS = [
+    0x726FDB47DD0E0E31, 0x74F839C593DC67FD, 0x0D6C8009D9A94F5A, 0x85676696D7FB7E2D,
+    0xCF2794E0277187B7, 0x18765564CD99A68D, 0xCBC9466E58FEE3CE, 0xAB0200F58B01D137,
+    0x93F5F5799A932462, 0x9E0082DF0BA9E4B0, 0x7A5DBBC594DDB9F3, 0xF4B32F46226BADA7,
+    0x751E8FBC860EE5FB, 0x14EA5627C0843D90, 0xF723CA908E7AF2EE, 0xA129CA6149BE45E5,
+]
+
+
 def test_siphash24_reference_vectors():
-    # SipHash paper vectors: key 00..0f, message 00..(n-1)
     k0, k1 = struct.unpack("<QQ", bytes(range(16)))
-    assert po.siphash(b"", k0, k1, 2, 4) == 0x726FDB47DD0E0E31
-    assert po.siphash(bytes(range(1)), k0, k1, 2, 4) == 0x74F839C593DC67FD
-    assert po.siphash(bytes(range(15)), k0, k1, 2, 4) == 0xA129CA6149BE45E5
     L = co.lib()
+    for n, want in enumerate(SIPHASH24_VECTORS):
+        m = bytes(range(n))
+        buf = (co.C.c_uint8 * max(1, n)).from_buffer_copy(m or b"\0")
+        assert po.siphash(m, k0, k1, 2, 4) == want, n
+        assert L.orc_siphash(buf, n, k0, k1, 2, 4) == want, n
     for n in (0, 1, 7, 8, 9, 15, 16, 63):
         m = bytes(range(n))
         buf = (co.C.c_uint8 * max(1, n)).from_buffer_copy(m or b"\0")
