@@ -16,9 +16,11 @@ def h(x):
 
 # ---------------------------------------------------------------- primitives vs published vectors
 def test_chacha20_zero_key_keystream():
-    # DJB ChaCha20, key = 0, nonce = 0, block 0: 76 b8 e0 ad a0 f1 3d 90 ...
+    # DJB ChaCha20, key = 0, nonce = 0, block 0: the whole 64-byte keystream block
     w = po.chacha20_block([0] * 8, 0)
-    assert w[:4] == [0xADE0B876, 0x903DF1A0, 0xE56A5D40, 0x28BD8653]
+    assert b"".join(x.to_bytes(4, "little") for x in w) == bytes.fromhex(
+        "76b8e0ada0f13d90405d6ae55386bd28bdd219b8a08ded1aa836efcc8b770dc7"
+        "da41597c5157488d7724e03fb8d84a376a43b8f41518a11cc387b669b2ee6586")
     out = (co.C.c_uint32 * 16)()
     co.lib().orc_chacha20_block((co.C.c_uint32 * 8)(*[0] * 8), co.C.c_uint64(0), out)
     assert list(out) == w
@@ -29,7 +31,9 @@ def test_chacha20_rfc8439_block():
     key = list(struct.unpack("<8I", bytes(range(32))))
     st = [0x61707865, 0x3320646E, 0x79622D32, 0x6B206574] + key + [1, 0x09000000, 0x4A000000, 0]
     out = po.chacha20_block_raw(st)
-    assert out[:4] == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3]
+    assert out == [0xE4E7F110, 0x15593BD1, 0x1FDD0F50, 0xC47120A3, 0xC7F4D1C7, 0x0368C033, 0x9AAA2204,
+                   0x4E6CD4C3, 0x466482D2, 0x09AA9F07, 0x05D7C214, 0xA2028BD9, 0xD19C12B5, 0xB94E16DE,
+                   0xE883D0CB, 0x4E3C50A2]
 
 
 # SipHash-2-4 reference-implementation vectors (key 00..0f, message 00..(n-1)), n = 0..15: every
