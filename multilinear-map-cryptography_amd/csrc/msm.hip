@@ -1070,6 +1070,33 @@ static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
     k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb, acc_k,
                                                         !(hv && hv[0] == '0'));
     TNS_LAUNCH_CHECK();
+    if (const char *fs = getenv("TNS_FIX_STATS"); fs && fs[0] == '1') {  // diagnostics: the runs' chunk spans
+      std::vector<uint32_t> bs(P.nb + 1);
+      uint32_t nvalid = 0;
+      TNS_HIP(hipStreamSynchronize(st));
+      TNS_HIP(hipMemcpy(bs.data(), bstart, sizeof(uint32_t) * (P.nb + 1), hipMemcpyDeviceToHost));
+      TNS_HIP(hipMemcpy(&nvalid, valid, sizeof(uint32_t), hipMemcpyDeviceToHost));
+      size_t cls[7] = {0}, maxspan = 0, maxent = 0, heavy_waves = 0, max_heavy_in_wave = 0;
+      for (size_t w = 0; w * 64 < P.nb; w++) {
+        size_t hw = 0;
+        for (size_t bk = w * 64; bk < std::min(P.nb, w * 64 + 64); bk++) {
+          const uint32_t s = bs[bk], e = bs[bk + 1];
+          const size_t tf = s / acc_k, tl = e > s ? (e - 1) / acc_k : tf, sp = tl - tf;
+          maxspan = std::max(maxspan, sp);
+          maxent = std::max<size_t>(maxent, e - s);
+          cls[s == e ? 0 : sp == 0 ? 1 : sp == 1 ? 2 : sp < 8 ? 3 : sp < 64 ? 4 : sp <= FIX_WAVE_SPAN ? 5 : 6]++;
+          hw += sp > FIX_WAVE_SPAN;
+        }
+        heavy_waves += hw > 0;
+        max_heavy_in_wave = std::max(max_heavy_in_wave, hw);
+      }
+      fprintf(stderr,
+              "[fix-stats] nb %zu entries %u acc_k %d chunks %zu levels %d | empty %zu in-chunk %zu span1 %zu "
+              "span2-7 %zu span8-63 %zu span64-%zu %zu heavy %zu | max span %zu max entries %zu heavy waves %zu "
+              "max heavy per wave %zu\n",
+              P.nb, nvalid, acc_k, nchunks, F.n, cls[0], cls[1], cls[2], cls[3], cls[4], FIX_WAVE_SPAN, cls[5],
+              cls[6], maxspan, maxent, heavy_waves, max_heavy_in_wave);
+    }
   }
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
   // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
