@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "common.hpp"
@@ -902,7 +903,15 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
     bits[p] = (rest + (npass - 2 - p)) / (npass - 1 - p);
     rest -= bits[p];
   }
-  if (const char *e = getenv("TNS_BS_BITS")) {  // tuning: "b0,b1,..." (each <= 9, summing to keybits)
+  const char *bbe = getenv("TNS_BS_BITS");
+  if (bbe && !strcmp(bbe, "last+1")) {  // (tests) one bit moved from the first pass to the last
+    if (npass >= 2 && bits[npass - 1] < BS_LASTBITS && bits[0] >= 2) {
+      bits[0]--;
+      bits[npass - 1]++;
+      J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 &&
+             bits[npass - 1] >= J.wb;
+    }
+  } else if (const char *e = bbe) {  // tuning: "b0,b1,..." (each <= 9, the last <= 10, summing to keybits)
     int v[8], k = 0, sum = 0;
     for (const char *q = e; *q && k < 8;) {
       v[k] = atoi(q);
