@@ -878,6 +878,12 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
   return R;
 }
 
+// an integer sum-check knob from the environment (A/B and tests), else the default
+static int sc_env(const char *name, int dflt) {
+  const char *e = getenv(name);
+  return e && *e ? atoi(e) : dflt;
+}
+
 // one round's launch (tables already in kernel order); returns the flag value to wait for
 template <bool FOLD, bool SKIP1>
 static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P) {
@@ -886,10 +892,9 @@ static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P) {
   // workgroups, each thread looping over pairs
   const uint32_t seq = ++R.c->sc_seq;
   hipStream_t st = R.c->stream;
-  static const size_t split_max = [] {  // (TNS_SC_SPLIT_LOG: A/B of the split kernel's range)
-    const char *e = getenv("TNS_SC_SPLIT_LOG");
-    return e ? (size_t)1 << atoi(e) : (size_t)1 << 13;
-  }();
+  // (TNS_SC_SPLIT_LOG: A/B of the split kernel's range; the sum-check knobs are read per call, so
+  // a test can set them in-process)
+  const size_t split_max = (size_t)1 << sc_env("TNS_SC_SPLIT_LOG", 13);
   if (P <= split_max) {  // four lanes a pair, 16 pairs a one-wave block (2^12-2^14 measured alike;
                          // at 2^16 the pairs-per-lane kernel is 2x faster)
     const unsigned g = grid_for(P, 16, R.max_grid * 4);
@@ -963,10 +968,7 @@ Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Sumc
 static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                                  const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                                  Fr *challenges, Fr *final_vals, Fr *final_eval) {
-  static const bool prequeue = [] {
-    const char *e = getenv("TNS_SC_PREQUEUE");
-    return !(e && e[0] == '0');
-  }();
+  const bool prequeue = sc_env("TNS_SC_PREQUEUE", 1) != 0;
   const size_t n = (size_t)1 << nv;
   Fr *bufB[MAX_SC_TABLES], *bufC[MAX_SC_TABLES];
   for (int i = 0; i < k; i++) {
@@ -984,10 +986,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
   c->sc_chal_seq += nv + 1;
   R.chal->flag = 0;  // (no stale value can match: chal_base + i is fresh)
   // the persistent tail (k_sc_tail) from the first round r0 >= 2 of <= 2^tail_log pairs
-  static const unsigned tail_log = [] {  // TNS_SC_TAIL_LOG: its range (0: no tail kernel, A/B)
-    const char *e = getenv("TNS_SC_TAIL_LOG");
-    return e ? (unsigned)atoi(e) : 13u;
-  }();
+  const unsigned tail_log = (unsigned)sc_env("TNS_SC_TAIL_LOG", 13);  // its range (0: no tail kernel, A/B)
   unsigned r0 = nv;
   if (tail_log > 0)
     for (unsigned rr = 2; rr < nv; rr++)
@@ -1010,10 +1009,8 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
         }
         tail_seq = c->sc_seq + 1;
         c->sc_seq += nv - r0 + 1;
-        static const size_t gmax = [] {  // TNS_SC_TAIL_BLOCKS: the tail's one-wave blocks at most (A/B)
-          const char *e = getenv("TNS_SC_TAIL_BLOCKS");
-          return e ? (size_t)std::max(1, atoi(e)) : (size_t)64;  // 16 / 32 / 64 / 256 / 1024 measured
-        }();
+        // TNS_SC_TAIL_BLOCKS: the tail's one-wave blocks at most (A/B; 16 / 32 / 64 / 256 / 1024 measured)
+        const size_t gmax = (size_t)std::max(1, sc_env("TNS_SC_TAIL_BLOCKS", 64));
         const unsigned g = (unsigned)std::min<size_t>(gmax, std::max<size_t>(1, (n >> (r0 + 1)) / 16));
 #define TNS_SC_K(K)                                                                                             \
   k_sc_tail<K><<<g, 64, 0, c->stream>>>(pp, R.q_dev, r0, nv, n, R.chal_dev, chal_base, R.res_dev, tail_seq, \
