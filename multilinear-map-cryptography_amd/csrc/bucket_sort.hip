@@ -1022,10 +1022,8 @@ void bucket_sort_passes(BucketSortJob &J) {
     // low-magnitude buckets' segments multi-tile).  All one-tile: no geometry at all (at 2^24
     // the full layout's histograms and scan over 512 bins x every tile took 0.34 ms).
     J.last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
-    static const bool geom1 = [] {  // TNS_BS_GEOM=0: k_bs_tiles + scans (A/B)
-      const char *e = getenv("TNS_BS_GEOM");
-      return !(e && e[0] == '0');
-    }();
+    const char *ge = getenv("TNS_BS_GEOM");  // =0: k_bs_tiles + scans (A/B, a parity variant)
+    const bool geom1 = !(ge && ge[0] == '0');
     if (geom1 && J.S + 1 <= SCAN_SMALL) {
       uint32_t *pub = nullptr, *flag = nullptr, seq = 0;
       if (J.last && !lane_sync_readback()) lane_publish_slot(ln, LANE_SLOT_SORT, &pub, &flag, &seq);

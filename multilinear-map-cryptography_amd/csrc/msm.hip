@@ -758,12 +758,9 @@ __global__ void __launch_bounds__(256) k_lane_publish(PubArgs a, uint32_t *dst, 
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-bool lane_sync_readback() {
-  static const bool v = [] {
-    const char *e = getenv("TNS_MSM_SYNC_READBACK");
-    return e && e[0] == '1';
-  }();
-  return v;
+bool lane_sync_readback() {  // (read per call: the parity tests switch it in-process)
+  const char *e = getenv("TNS_MSM_SYNC_READBACK");
+  return e && e[0] == '1';
 }
 
 void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const size_t *bytes) {

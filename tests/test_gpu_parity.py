@@ -164,7 +164,8 @@ def test_msm_window_tables_equal_per_window_layout(logn):
 
 @pytest.mark.parametrize("variant", ["TNS_BS_RUNTIME_PASS1", "TNS_BS_NO_LOCAL_LAST", "TNS_MSM_W1", "TNS_FIX_WAVES",
                                      "TNS_BS_TILES", "TNS_MASKED_TREE", "TNS_ACC_ROUNDS", "TNS_BS_PACK", "TNS_BS_VO", "TNS_BS_K16",
-                                     "TNS_BS_K16=2", "TNS_RED_L1=0", "TNS_RED_L1=8", "TNS_BS_BITS=last+1"])
+                                     "TNS_BS_K16=2", "TNS_RED_L1=0", "TNS_RED_L1=8", "TNS_BS_BITS=last+1",
+                                     "TNS_BS_GEOM=0", "TNS_MSM_SYNC_READBACK=1"])
 @pytest.mark.parametrize("pattern", ["full", "addr21", "addr22", "val30", "equal"])
 def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     """The bucket sort's fast paths == its general kernels: the compile-time-plan pass 1 (c = 20,
@@ -185,7 +186,9 @@ def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
     the bucket reduction's second level (k_reduce_level2, L1 = 4 by default) off (TNS_RED_L1=0:
     masked sums straight over the first level's groups) or with groups of 8, and one key bit moved
     from the first sort pass to the last (TNS_BS_BITS=last+1: a 9-bit last pass becomes the
-    1024-bin kernels)."""
+    1024-bin kernels), and the sort geometry as tile counts + scans instead of one launch
+    (TNS_BS_GEOM=0) and the MSM's host readbacks as pinned copies + a stream synchronize instead of
+    the published flag (TNS_MSM_SYNC_READBACK=1)."""
     pp, _ = params(18)
     n = 1 << 20
     rng = np.random.default_rng(len(pattern))
