@@ -1032,7 +1032,8 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     }
     ScTables tt{};
     if (rr == nv) {
-      for (int m = 0; m < k; m++) tt.in[m] = nv == 1 ? tables[R.perm[m]] : out_of(nv - 1, m);
+      // nv <= 1: the caller's tables (nv == 0 reads them as they are; nv - 1 would wrap)
+      for (int m = 0; m < k; m++) tt.in[m] = nv <= 1 ? tables[R.perm[m]] : out_of(nv - 1, m);
       const uint32_t seq = ++c->sc_seq;
       k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, R.rd, nv > 0, R.res_dev, seq);
       TNS_LAUNCH_CHECK();
