@@ -165,10 +165,12 @@ int tns_ctx_set_commit_basis(tns_ctx *ctx, int lagrange);
  * nothing is cached -- no error is returned for a table.  Setting 0 here before the first MSM
  * keeps every table from being built. */
 int tns_ctx_set_msm_tables(tns_ctx *ctx, int on);
-/* The MSM's bucket order: rocprim != 0 uses a digit array + rocPRIM radix sort instead of the
- * fused digit/counting sort (default; TNS_MSM_SORT=cub at context creation does the same).
- * Same results; A/B and test use. */
-int tns_ctx_set_msm_sort(tns_ctx *ctx, int rocprim);
+/* Drop-in provers (tns_twist_prove on host buffers): the value vector crosses PCIe in `chunks`
+ * equal node ranges (1..64, default 4), each committed by its own MSM as soon as it lands, so only
+ * the last range's MSM follows the link (C4: commit phase 19.0 -> 15.5 ms at 4).  Same proofs
+ * for every setting; out of range -> TNS_ERR_INVALID_PARAMETERS.  The library reads no tuning
+ * from the environment: this and the two setters above are its whole tuning surface. */
+int tns_ctx_set_upload_chunks(tns_ctx *ctx, int chunks);
 
 /* ---------------------------------------------------------------- KZG (src/commitments.rs) */
 /* CommitmentScheme::commit for KZGCommitment (src/commitments.rs:162-180).
@@ -345,6 +347,8 @@ int tns_comm_set_timeout(tns_comm *comm, double seconds);
 /* out = {exchange steps so far, their total seconds, the longest one's seconds, the deadline}
  * (multi-rank communicators; timed on the host around each allgather). */
 int tns_comm_stats(const tns_comm *comm, double out[4]);
+/* tns_comm_stats + {bytes this rank sent over all exchange steps, the largest step's bytes}. */
+int tns_comm_stats_ex(const tns_comm *comm, double out[6]);
 /* Build (and cache) rank `rank` of `size`'s slice of the Lagrange basis for N = 2^k nodes
  * ahead of the first sharded proof of that size (setup, like tns_srs_prepare_lagrange). */
 int tns_srs_prepare_lagrange_shard(tns_ctx *ctx, tns_srs *srs, size_t n, int rank, int size);

@@ -191,27 +191,55 @@ static G1Xyzz sum_rank_parts(const G1Xyzz *all, int size, int stride, int k) {
   return acc;
 }
 
-static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affine out[2], const char *what) {
+// What rides along with an exchange of MSM partials (the exchanges of a sharded proof are few and
+// latency-bound, so independent payloads share one): `bytes` of this rank's data, every rank's
+// copy landing rank-major in `all` (size * bytes).
+struct ExtraPayload {
+  const void *data = nullptr;
+  size_t bytes = 0;  // a multiple of 4
+  std::vector<uint8_t> all;
+};
+
+static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affine out[2], const char *what,
+                                  ExtraPayload *extra = nullptr) {
+  const size_t xb = extra ? extra->bytes : 0;
   if (m.size == 1) {
     out[0] = xyzz_to_affine(part[0]);
     out[1] = xyzz_to_affine(part[1]);
+    if (xb) extra->all.assign((const uint8_t *)extra->data, (const uint8_t *)extra->data + xb);
     return;
   }
-  std::vector<G1Xyzz> all(2 * (size_t)m.size);
-  m.exchange(c, part, 2 * sizeof(G1Xyzz), all.data(), what);
-  out[0] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 0));
-  out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, 2, 1));
+  // one message per rank: [partial 0 | partial 1 | extra], G1Xyzz-aligned
+  const size_t rec = 2 * sizeof(G1Xyzz) + (xb + sizeof(G1Xyzz) - 1) / sizeof(G1Xyzz) * sizeof(G1Xyzz);
+  const size_t recw = rec / sizeof(G1Xyzz);
+  std::vector<G1Xyzz> mine(recw), all(recw * (size_t)m.size);
+  mine[0] = part[0];
+  mine[1] = part[1];
+  if (xb) std::memcpy(&mine[2], extra->data, xb);
+  m.exchange(c, mine.data(), rec, all.data(), what);
+  out[0] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, (int)recw, 0));
+  out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, (int)recw, 1));
+  if (xb) {
+    extra->all.resize(xb * (size_t)m.size);
+    for (int r = 0; r < m.size; r++)
+      std::memcpy(extra->all.data() + xb * (size_t)r, &all[recw * (size_t)r + 2], xb);
+  }
 }
 
 // src0 / src1 (optional): how p0.y / p1.y get written (on the MSM lane that reads them)
+// extra (optional, sharded): data exchanged with the commitments' partial sums
 static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, Comm &m, G1Affine out[2],
-                              const ScalarSource *src0 = nullptr, const ScalarSource *src1 = nullptr) {
+                              const ScalarSource *src0 = nullptr, const ScalarSource *src1 = nullptr,
+                              ExtraPayload *extra = nullptr) {
   if (p0.N > srs.n || p1.N > srs.n) throw Error(TNS_ERR_COMMITMENT, "Polynomial degree exceeds setup size");
   p0.basis = lagrange_basis_dev(c, srs, p0.N, p0.first, p0.cnt);
   p1.basis = lagrange_basis_dev(c, srs, p1.N, p1.first, p1.cnt);
   if (!p0.basis || !p1.basis) {
     for (const ScalarSource *s : {src0, src1})
       if (s && s->prep) s->prep(c->stream);
+    if (extra && extra->bytes && m.size > 1)  // (the coefficient route is unsharded: never taken here)
+      throw Error(TNS_ERR_PROOF_GENERATION, "sharded commitment without a Lagrange basis");
+    if (extra) extra->all.assign((const uint8_t *)extra->data, (const uint8_t *)extra->data + extra->bytes);
     out[0] = commit_evals(c, srs, p0, m);
     out[1] = commit_evals(c, srs, p1, m);
     return;
@@ -233,17 +261,21 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
   };
   G1Xyzz part[2];
   msm_pair_dev(c, args(p0, src0), args(p1, src1), part);
-  allgather_sum_g1_pair(c, m, part, out, "commitment pair partial MSMs");
+  allgather_sum_g1_pair(c, m, part, out, "commitment pair partial MSMs", extra);
 }
 
-// after_quotients (optional): called once the quotient kernel is queued (the side-stream folds'
-// placement A/B, TNS_FOLDS_AT=1)
+// extra (optional): exchanged with the openings' partial sums once extra_ready() has run (the
+// sharded sum-check's folded table values, which the side stream computes under the openings)
 static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, const Fr &z, Fr value[2],
                             G1Affine proof[2], DevBuf &sbuf0, DevBuf &sbuf1, Comm &m,
-                            const std::function<void()> &after_quotients = nullptr) {
+                            ExtraPayload *extra = nullptr, const std::function<void()> &extra_ready = nullptr) {
   if (!p0.basis || !p1.basis || fr_is_node(z, p0.N) || fr_is_node(z, p1.N)) {
     open_evals(c, srs, p0, z, &value[0], &proof[0], sbuf0, m);
     open_evals(c, srs, p1, z, &value[1], &proof[1], sbuf0, m);
+    if (extra) {  // (unsharded here: open_evals refuses a node z with several ranks)
+      if (extra_ready) extra_ready();
+      extra->all.assign((const uint8_t *)extra->data, (const uint8_t *)extra->data + extra->bytes);
+    }
     return;
   }
   Fr *q0 = (Fr *)sbuf0.ensure(sizeof(Fr) * p0.cnt), *q1 = (Fr *)sbuf1.ensure(sizeof(Fr) * p1.cnt);
@@ -251,12 +283,8 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
   const bool same_nodes = p0.N == p1.N && p0.first == p1.first && p0.cnt == p1.cnt;
   // the shared-inverse pass hands the MSMs canonical quotients and their bit lengths; its
   // inverses come out canonical too, so the quotient kernel needs no reduction pass
-  // (TNS_CANON_INV=0: Montgomery inverses and a from_mont per quotient, A/B)
-  static const bool canon_env = [] {
-    const char *e = getenv("TNS_CANON_INV");
-    return !(e && e[0] == '0');
-  }();
-  const bool canon_q = same_nodes && p0.cnt > 64, canon_inv = canon_q && canon_env;
+  // (0.540 -> 0.504 ms at C4, profiles/r04_c4_step_timeline_canon_inv.txt)
+  const bool canon_q = same_nodes && p0.cnt > 64, canon_inv = canon_q;
   if (same_nodes) {  // Twist: one batch inversion for both vectors (inverses land in q1)
     Fr p3[3];
     lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3, canon_inv);
@@ -282,11 +310,12 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
     lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
     lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
   }
-  if (after_quotients) after_quotients();
   G1Xyzz pp[2];
   msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits},
                MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr}, pp);
-  allgather_sum_g1_pair(c, m, pp, proof, "opening pair partial MSMs");
+  if (extra && extra_ready) extra_ready();
+  allgather_sum_g1_pair(c, m, pp, proof, extra ? "opening pair partial MSMs + folded table values" : "opening pair partial MSMs",
+                        extra);
 }
 
 // shard geometry: `size` ranks over N padded entries (size a power of two <= N)
@@ -371,21 +400,9 @@ int tns_ctx_create(int device, tns_ctx **out) {
     x->c.lanes[0].stream = x->c.stream;
     int prio_lo = 0, prio_hi = 0;
     TNS_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    const char *st = getenv("TNS_MSM_STAGGER");
-    x->c.msm_stagger = st && st[0] == '1';
     x->c.num_cu = prop.multiProcessorCount;
-    if (const char *aw = getenv("TNS_ACC_WAVES")) x->c.acc_waves = atoi(aw);
-    if (const char *ak = getenv("TNS_ACC_K")) x->c.acc_k = std::max(1, atoi(ak));
-    if (const char *at = getenv("TNS_ACC_THREADS_CU")) x->c.acc_threads_cu = std::max(1, atoi(at));
-    if (const char *rl = getenv("TNS_RED_L")) x->c.red_l = std::max(0, atoi(rl));
-    if (const char *rc = getenv("TNS_RED_CH")) x->c.red_ch = std::max(0, atoi(rc));
-    if (const char *sc = getenv("TNS_SC_TAIL")) x->c.sc_tail = sc[0] != '0';
-    if (const char *mc = getenv("TNS_MSM_C")) x->c.msm_c = std::max(0, std::min(20, atoi(mc)));
-    if (const char *se = getenv("TNS_MSM_SERIAL")) x->c.msm_serial = se[0] != '0';
-    const char *cs = getenv("TNS_MSM_SORT");
-    x->c.msm_cub_sort = cs && std::string(cs) == "cub";
-    TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking,
-                                        x->c.msm_stagger ? prio_hi : prio_lo));
+    (void)prio_hi;
+    TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking, prio_lo));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.copy, hipStreamNonBlocking));
     *out = x;
@@ -597,10 +614,12 @@ int tns_ctx_set_msm_tables(tns_ctx *ctx, int on) {
   });
 }
 
-int tns_ctx_set_msm_sort(tns_ctx *ctx, int rocprim) {
+int tns_ctx_set_upload_chunks(tns_ctx *ctx, int chunks) {
   return guarded([&]() {
+    if (!ctx) throw Error(TNS_ERR_INVALID_PARAMETERS, "null context");
+    if (chunks < 1 || chunks > 64) throw Error(TNS_ERR_INVALID_PARAMETERS, "upload chunks must be 1..64");
     CtxScope g(&ctx->c);
-    ctx->c.msm_cub_sort = rocprim != 0;
+    ctx->c.upload_chunks = chunks;
     return TNS_OK;
   });
 }
@@ -920,11 +939,10 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   // ... and the folds binding this rank's tables at r_0 .. r_{nv_loc-1} (the MLE values the
   // closure evaluates, src/sumcheck.rs:104) run on the side stream under the openings; their
   // values are collected at the end of the proof
+  // (queued behind the quotient kernel instead, under the opening sorts: a tie, 49.19-49.51 vs
+  // 49.32-49.51 ms per step, profiles/r04_ab_folds_at.txt)
   Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
-  bool folds_queued = false;
-  auto queue_folds = [&]() {
-    if (folds_queued) return;
-    folds_queued = true;
+  {
     hipEvent_t ready;
     TNS_HIP(hipEventCreateWithFlags(&ready, hipEventDisableTiming));
     TNS_HIP(hipEventRecord(ready, c->stream));  // the tables were written on the context stream
@@ -932,14 +950,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     (void)hipEventDestroy(ready);
     sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals, flags, n_flags);
     TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
-  };
-  // TNS_FOLDS_AT=1 (A/B): queue the folds behind the quotient kernel, i.e. under the opening
-  // sorts instead of beside the barycentric pass
-  static const int folds_at = [] {
-    const char *e = getenv("TNS_FOLDS_AT");
-    return e ? atoi(e) : 0;
-  }();
-  if (folds_at != 1 || nv < 1) queue_folds();
+  }
   const Fr fe = Fr::zero();
   out->num_rounds = nv;
   std::memcpy(out->round_polynomials, rounds.data(), 128 * (size_t)nv);
@@ -951,12 +962,23 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   // that nothing reads afterwards, so they are not derived (no observable output depends on
   // them; ~0.1 ms of host hashing in front of the openings at nv = 24)
   Timer t_open;
+  // sharded: every rank's folded values travel with the opening partials (one exchange, not two)
+  Fr finals[3];
+  ExtraPayload fold_x;
+  fold_x.data = finals;
+  fold_x.bytes = sizeof(Fr) * (size_t)n_mles;
+  bool folds_exchanged = false;
+  auto folds_ready = [&]() {
+    TNS_HIP(hipStreamSynchronize(c->side));
+    for (int j = 0; j < n_mles; j++) finals[j] = vals[j];
+  };
   if (nv >= 1) {
     Fr z = tr.challenge("opening_challenges_0");
     std::memcpy(out->opening_point, &z, 32);
     Fr v[2];
     G1Affine pi[2];
-    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m, queue_folds);
+    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m, lr ? &fold_x : nullptr, folds_ready);
+    folds_exchanged = lr > 0;
     store_proj(pi[0], out->opening_proofs[0]);
     store_proj(pi[1], out->opening_proofs[1]);
     std::memcpy(out->final_evaluations[0], &v[0], 32);
@@ -964,14 +986,13 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     out->num_openings = 2;
   }
   timing[4] = t_open.ms();
-  queue_folds();  // (a no-op unless the openings took a path without the hook)
   // the side stream's bound table values; with several ranks each holds its slice's values at
   // r_0 .. r_{nv_loc-1}, and the last lr challenges fold the allgathered rank values
-  TNS_HIP(hipStreamSynchronize(c->side));
-  Fr finals[3];
-  for (int j = 0; j < n_mles; j++) finals[j] = vals[j];
+  folds_ready();
   if (lr) {
-    const std::vector<Fr> all = allgather_fr(c, m, finals, (size_t)n_mles, "sum-check folded table values");  // rank-major
+    std::vector<Fr> all((size_t)n_mles * m.size);  // rank-major
+    if (folds_exchanged) std::memcpy(all.data(), fold_x.all.data(), sizeof(Fr) * all.size());
+    else all = allgather_fr(c, m, finals, (size_t)n_mles, "sum-check folded table values");
     for (int j = 0; j < n_mles; j++) {
       std::vector<Fr> t(m.size);
       for (int r = 0; r < m.size; r++) t[r] = all[(size_t)r * n_mles + j];
@@ -1000,27 +1021,13 @@ __global__ void k_max_index_check(const uint64_t *__restrict__ idx, size_t n, ui
 // On every exit of a prove call (an exception included): nothing this call queued on the side
 // stream (the flag table, the zero-closure folds: they read the caller's value / is_write
 // buffers in the device-resident entry points) is still running when the call returns.
-// node ranges the drop-in provers upload (and commit) the late vector in (TNS_UPLOAD_CHUNKS)
-static int upload_chunks() {
-  const char *e = getenv("TNS_UPLOAD_CHUNKS");
-  const int k = e ? atoi(e) : 4;
-  return std::max(1, std::min(64, k));
-}
-
-// The node ranges the drop-in values arrive in: k equal ranges; TNS_UPLOAD_SPLIT_LAST=1 splits
-// the last one in two halves, so the MSM left after the upload is an eighth of the vector
-// instead of a quarter -- measured equal at C4 (56.4-57.5 vs 56.4-57.9 ms per drop-in proof,
-// profiles/r04_ab_upload_split.txt: the last chunk's fixed tail dominates), so not the default.
+// The node ranges the drop-in values arrive in: k equal ranges (Ctx::upload_chunks).  (Splitting the
+// last one in two, so the MSM left after the upload is an eighth of the vector, measured equal at
+// C4: 56.4-57.5 vs 56.4-57.9 ms per drop-in proof, profiles/r04_ab_upload_split.txt.)
 static std::vector<size_t> upload_chunk_offsets(size_t n, int k) {
   std::vector<size_t> off;
   const size_t per = (n + k - 1) / std::max(k, 1);
   for (size_t o = 0; o < n; o += per) off.push_back(o);
-  const char *e = getenv("TNS_UPLOAD_SPLIT_LAST");
-  const bool split = e && e[0] == '1';
-  if (split && off.size() > 1) {
-    const size_t last = off.back(), len = n - last;
-    if (len >= 2) off.push_back(last + len / 2);
-  }
   off.push_back(n);
   return off;
 }
@@ -1073,10 +1080,10 @@ static void twist_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
   // is `late` in commit_evals_pair and waits for it
   const bool v_late = kind == hipMemcpyHostToDevice && n_ops > 0;
   int up_a = -1, up_f = -1, up_v = -1;
-  // the values arrive in v_chunks node ranges, each committed as it lands (TNS_UPLOAD_CHUNKS,
+  // the values arrive in v_chunks node ranges, each committed as it lands (tns_ctx_set_upload_chunks,
   // default 4; 1 = one upload, one MSM after it); padded slices (L > n_ops) keep one MSM
   const std::vector<size_t> v_off =
-      upload_chunk_offsets(n_ops, v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? upload_chunks() : 1);
+      upload_chunk_offsets(n_ops, v_late && L == n_ops && n_ops >= ((size_t)1 << 18) ? c->upload_chunks : 1);
   const int v_chunks = std::max(1, (int)v_off.size() - 1);  // ranges actually formed
   uint32_t *dar32 = nullptr;
   // the op-type table is read by the sum-check only: its first fold pass reads the flag bytes
@@ -1268,12 +1275,10 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     TNS_HIP(hipMemcpyAsync(&hbad, bad, sizeof hbad, hipMemcpyDeviceToHost, st));
     TNS_HIP(hipStreamSynchronize(st));
   }
-  if (m.size > 1) {
-    std::vector<unsigned> flags(m.size);
-    m.exchange(c, &hbad, sizeof hbad, flags.data(), "input validity flags");
-    for (unsigned f : flags) hbad |= f;
-  }
-  if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
+  // (sharded: every rank's verdict travels with the commitments' partial sums and all ranks fail
+  // together after that exchange -- the MSMs read the indices as scalars only, so an out-of-range
+  // index is harmless until then, and a rank failing alone here would leave its peers waiting)
+  if (hbad && m.size == 1) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
   if (kind == hipMemcpyHostToDevice) TNS_HIP(hipStreamSynchronize(st));
   tm[0] = t_h2d.ms();
   // the index table is written on lane 1 as the index commitment starts (see twist_core)
@@ -1303,8 +1308,20 @@ static void shout_core(tns_ctx *ctx, const tns_srs *srs, const tns_params *param
     src_t.prep = [&upload, up_t](hipStream_t s) { upload.wait(up_t, s); };
     src_t.late = true;
   }
-  commit_evals_pair(c, srs->s, pt, pi, m, cm, t_late ? &src_t : nullptr, &src_i);  // (src/shout.rs:125-133)
+  ExtraPayload bad_x;
+  bad_x.data = &hbad;
+  bad_x.bytes = sizeof hbad;
+  commit_evals_pair(c, srs->s, pt, pi, m, cm, t_late ? &src_t : nullptr, &src_i,
+                    m.size > 1 ? &bad_x : nullptr);  // (src/shout.rs:125-133)
   if (up_t >= 0) upload.wait_all(st);
+  if (m.size > 1) {  // LookupTable::lookup bounds (src/shout.rs:44-50), agreed over the ranks
+    for (int r = 0; r < m.size; r++) {
+      unsigned f;
+      std::memcpy(&f, bad_x.all.data() + sizeof f * (size_t)r, sizeof f);
+      hbad |= f;
+    }
+    if (hbad) throw Error(TNS_ERR_INVALID_PARAMETERS, "Lookup index out of bounds");
+  }
   const G1Affine Ct = cm[0], Ci = cm[1];
   store_proj(Ct, out->commitments[0]);
   store_proj(Ci, out->commitments[1]);
@@ -1648,6 +1665,19 @@ int tns_comm_set_timeout(tns_comm *comm, double seconds) {
     if (!comm || !comm->c) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator");
     if (!(seconds > 0.0)) throw Error(TNS_ERR_INVALID_PARAMETERS, "timeout must be positive");
     comm->c->timeout_s = seconds;
+    return TNS_OK;
+  });
+}
+
+int tns_comm_stats_ex(const tns_comm *comm, double out[6]) {
+  return guarded([&]() {
+    if (!comm || !comm->c || !out) throw Error(TNS_ERR_INVALID_PARAMETERS, "null communicator or output");
+    out[0] = (double)comm->c->seq;
+    out[1] = comm->c->total_s;
+    out[2] = comm->c->max_s;
+    out[3] = comm->c->timeout_s;
+    out[4] = comm->c->bytes_total;
+    out[5] = comm->c->bytes_max;
     return TNS_OK;
   });
 }

@@ -36,17 +36,10 @@ namespace tns {
 constexpr int BS_BLOCK = TNS_BS_BLOCK;  // 4 waves: fits the slots k_accumulate leaves free
 constexpr int BS_MAXBITS = 9;  // key bits per pass
 constexpr int BS_MAXBINS = 1 << BS_MAXBITS;
-// the last pass may take one bit more (TNS_BS_BITS, e.g. 8,7,10: its segments stay one tile, and
-// the earlier passes get fewer bins, i.e. longer write runs): its kernels hold 1024 bins
-constexpr int BS_LASTBITS = 10;
-constexpr int BS_LASTBINS = 1 << BS_LASTBITS;
 #ifndef TNS_BS_TILE_MAX
 #define TNS_BS_TILE_MAX 8192
 #endif
 constexpr int BS_TILE = TNS_BS_TILE_MAX;  // entries per tile at most (LDS staging: 8 B each, 64 KiB at 8192)
-// the tile of sorts that run beside an MSM accumulation (BucketSortJob::corun): 8 entries per
-// thread, so the scatter kernels stay within the registers the accumulation leaves free
-constexpr int BS_CORUN_TILE = 2048;
 // per-pass tile sizes (template parameter TILE of the scatter kernels): 8192 or 4096 entries
 constexpr int BS_SCALARS = 4;  // scalars a pass-1 thread loads ahead
 
@@ -177,46 +170,29 @@ __device__ __forceinline__ void block_scan_bins(const uint32_t *h, uint32_t *out
 static_assert(BS_MAXBINS <= 2 * BS_BLOCK, "two bins per thread in the block scan");
 
 // Key formats between passes (BucketSortJob::kf): the keys a pass writes only need the key bits
-// the later passes still sort by.  KF_U32: 4-byte keys; KF_U16: 2-byte keys (<= 16 bits left);
-// KF_U16S: 17 bits left -- bits [1, 17) in 2 bytes, bit 0 in bit 30 of the value (values are
-// < 2^30 there, bit 31 is the sign).  The reader restores the key's low bits and the value.
-enum { KF_U32 = 0, KF_U16 = 1, KF_U16S = 2 };
-constexpr uint32_t BS_STASH = 0x40000000u;
+// the later passes still sort by.  KF_U32: 4-byte keys; KF_U16: 2-byte keys (<= 16 bits left: the
+// keys into the last pass, whose <= 9 key bits are all it reads).  (2-byte keys out of pass 1 too,
+// the 17th bit carried in the value, measured slower: pass 1 +0.2 ms, pass 2 +0.35 ms per 2^24
+// opening, their ~64-byte runs of half-dword stores costing more than the bytes saved.)
+enum { KF_U32 = 0, KF_U16 = 1 };
 
 __device__ __forceinline__ void store_entry(int kf, uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
                                             uint32_t pos, uint32_t key, uint32_t val) {
-  if (kf == KF_U32) {
-    okeys[pos] = key;
-    ovals[pos] = val;
-  } else if (kf == KF_U16) {
-    reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)key;
-    ovals[pos] = val;
-  } else {
-    reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)(key >> 1);
-    ovals[pos] = val | ((key & 1u) << 30);
-  }
+  if (kf == KF_U32) okeys[pos] = key;
+  else reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)key;
+  ovals[pos] = val;
 }
 
 // entry i's key (the low bits a pass still needs) and value in format kf
 __device__ __forceinline__ void load_entry(int kf, const uint32_t *__restrict__ keys, const uint32_t *__restrict__ vals,
                                            size_t i, uint32_t &key, uint32_t &val) {
   val = vals[i];
-  if (kf == KF_U32) {
-    key = keys[i];
-  } else {
-    key = reinterpret_cast<const uint16_t *>(keys)[i];
-    if (kf == KF_U16S) {
-      key = (key << 1) | ((val >> 30) & 1u);
-      val &= ~BS_STASH;
-    }
-  }
+  key = kf == KF_U32 ? keys[i] : (uint32_t)reinterpret_cast<const uint16_t *>(keys)[i];
 }
 
-// key only (histograms; KF_U16S without its bit 0: only passes with shift >= 1 read that format)
+// key only (histograms)
 __device__ __forceinline__ uint32_t load_key(int kf, const uint32_t *__restrict__ keys, size_t i) {
-  if (kf == KF_U32) return keys[i];
-  const uint32_t k = reinterpret_cast<const uint16_t *>(keys)[i];
-  return kf == KF_U16 ? k : k << 1;
+  return kf == KF_U32 ? keys[i] : (uint32_t)reinterpret_cast<const uint16_t *>(keys)[i];
 }
 
 // Tile writer: entries already placed in lk/lv by bin (bin d at [lbase[d], lbase[d] + cnt));
@@ -391,23 +367,21 @@ struct Pass1Plan {
   void (*count)(DigitArgs, int, int, size_t, uint32_t *);
   void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, int, uint32_t *, uint32_t *);
   int spt;
-  bool corun;  // a plan for sorts that run beside an accumulation (BucketSortJob::corun)
 };
-#define TNS_P1(T, C, W, SPT, CO) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT, CO}
+#define TNS_P1(T, C, W, SPT) {T, C, W, k_bs_count1_ct<C, W>, k_bs_scatter1_ct<T, C, W, SPT>, SPT}
 static const Pass1Plan kPass1Plans[] = {
-    TNS_P1(BS_TILE, 22, 12, 3, false), TNS_P1(BS_TILE, 20, 13, 3, false), TNS_P1(BS_TILE, 19, 14, 3, false),
-    TNS_P1(BS_TILE, 17, 15, 3, false), TNS_P1(BS_TILE, 16, 2, 16, false), TNS_P1(BS_TILE, 12, 2, 16, false),
-    // half tiles (half the LDS: twice the blocks per CU)
-    TNS_P1(4096, 22, 12, 2, false), TNS_P1(4096, 20, 13, 2, false),
-    // co-running sorts (BucketSortJob::corun): 2048-entry tiles, at most one scalar per thread
-    TNS_P1(BS_CORUN_TILE, 22, 12, 1, true), TNS_P1(BS_CORUN_TILE, 20, 13, 1, true)};
+    TNS_P1(BS_TILE, 22, 12, 3), TNS_P1(BS_TILE, 20, 13, 3), TNS_P1(BS_TILE, 19, 14, 3),
+    TNS_P1(BS_TILE, 17, 15, 3), TNS_P1(BS_TILE, 16, 2, 16), TNS_P1(BS_TILE, 12, 2, 16)};
 #undef TNS_P1
 
 // bins of pass 1 -> segment starts; seg[nbins] = total = number of entries (also *valid)
 __global__ void k_bs_segs1(const uint32_t *__restrict__ offs, int nbins, size_t T1, uint32_t *__restrict__ seg,
                            uint32_t *__restrict__ valid) {
   for (int d = threadIdx.x; d <= nbins; d += blockDim.x) seg[d] = offs[(size_t)d * T1];
-  if (threadIdx.x == 0) *valid = offs[(size_t)nbins * T1];
+  if (threadIdx.x == 0) {
+    valid[0] = offs[(size_t)nbins * T1];
+    valid[1] = 0;  // (k_accumulate sets it when a run crosses a chunk)
+  }
 }
 
 // tiles per segment
@@ -421,10 +395,19 @@ __global__ void k_bs_tiles(const uint32_t *__restrict__ seg, size_t S, uint32_t 
   }
 }
 
-// desc[tile_base[s] + k] = s for the tiles k of segment s
+// desc[tile_base[s] + k] = s for the tiles k of segment s: one thread per tile, a binary search of
+// the tile bases (a thread per segment walked up to ~3 K tiles of one segment: 0.18 ms at 2^24)
 __global__ void k_bs_desc(const uint32_t *__restrict__ tbase, size_t S, uint32_t *__restrict__ desc) {
-  for (size_t s = blockIdx.x * (size_t)blockDim.x + threadIdx.x; s < S; s += (size_t)gridDim.x * blockDim.x)
-    for (uint32_t g = tbase[s]; g < tbase[s + 1]; g++) desc[g] = (uint32_t)s;
+  const uint32_t ntiles = tbase[S];
+  for (size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x; g < ntiles; g += (size_t)gridDim.x * blockDim.x) {
+    size_t lo = 0, hi = S;  // the last s with tbase[s] <= g (empty segments repeat the next base)
+    while (hi - lo > 1) {
+      const size_t mid = (lo + hi) >> 1;
+      if (tbase[mid] <= g) lo = mid;
+      else hi = mid;
+    }
+    desc[g] = (uint32_t)lo;
+  }
 }
 
 struct PassGeom {
@@ -490,8 +473,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count(PassGeom G, size_t S, siz
     }
   };
   if (G.kin == KF_U32) loads(std::integral_constant<int, KF_U32>());
-  else if (G.kin == KF_U16) loads(std::integral_constant<int, KF_U16>());
-  else loads(std::integral_constant<int, KF_U16S>());
+  else loads(std::integral_constant<int, KF_U16>());
 #pragma unroll
   for (int j = 0; j < IPT; j++)
     if (a + threadIdx.x + (size_t)j * BS_BLOCK < e) atomicAdd(&h[(kk[j] >> G.shift) & G.mask], 1u);
@@ -564,8 +546,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     }
   };
   if (PK == 2 || G.kin == KF_U32) loads(std::integral_constant<int, KF_U32>());
-  else if (G.kin == KF_U16) loads(std::integral_constant<int, KF_U16>());
-  else loads(std::integral_constant<int, KF_U16S>());
+  else loads(std::integral_constant<int, KF_U16>());
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < IPT; j++)
@@ -630,6 +611,11 @@ __global__ void k_bs_bucket_starts(const uint32_t *__restrict__ seg, size_t nb, 
 // consecutive items), reduce -> one block scanning the tile sums -> apply; a single tile is one
 // launch.  Replaces rocPRIM's look-back scan (round 3: 432 library launches per step).
 constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+// The one-block kernels of the sort's geometry (k_scan_parts, k_scan_single, k_bs_geom) run while
+// the OTHER lane's scatter holds most of every CU: a 1024-thread block needs 16 free wave slots on
+// one CU and waited for that scatter to drain (0.44-0.52 ms per launch in the C4 timeline,
+// profiles/r06_c4_step_timeline_p1.txt), 256-thread blocks slip in beside it.
+constexpr int ONE_BLOCK = 256;
 
 // exclusive prefix of x over the block (NT threads); *sum = the block total.  lds: NT / 64 words
 template <int NT>
@@ -687,14 +673,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint32_t *__
 }
 
 // the tile sums, scanned in place by one block
-__global__ void __launch_bounds__(1024) k_scan_parts(uint32_t *__restrict__ part, size_t np) {
-  __shared__ uint32_t lds[1024 / 64];
+__global__ void __launch_bounds__(ONE_BLOCK) k_scan_parts(uint32_t *__restrict__ part, size_t np) {
+  __shared__ uint32_t lds[ONE_BLOCK / 64];
   uint32_t carry = 0;
-  for (size_t b0 = 0; b0 < np; b0 += 1024) {
+  for (size_t b0 = 0; b0 < np; b0 += ONE_BLOCK) {
     const size_t i = b0 + threadIdx.x;
     const uint32_t x = i < np ? part[i] : 0u;
     uint32_t tot;
-    const uint32_t pre = block_excl_scan<1024>(x, lds, tot);
+    const uint32_t pre = block_excl_scan<ONE_BLOCK>(x, lds, tot);
     if (i < np) part[i] = carry + pre;
     carry += tot;
   }
@@ -728,15 +714,15 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t *__r
   }
 }
 
-// up to SCAN_SMALL counts in ONE launch: one block of 1024 threads walks the array in rounds of
-// 1024 x 16 (the segment-count scans of the later passes: 257 .. 65 537 entries, where three
+// up to SCAN_SMALL counts in ONE launch: one block of ONE_BLOCK threads walks the array in rounds of
+// ONE_BLOCK x 16 (the segment-count scans of the later passes: 257 .. 65 537 entries, where three
 // launches of a few microseconds each were most of the cost)
 constexpr size_t SCAN_SMALL = (size_t)1 << 17;
-__global__ void __launch_bounds__(1024) k_scan_single(const uint32_t *__restrict__ in, size_t n,
+__global__ void __launch_bounds__(ONE_BLOCK) k_scan_single(const uint32_t *__restrict__ in, size_t n,
                                                       uint32_t *__restrict__ out) {
-  __shared__ uint32_t lds[1024 / 64];
+  __shared__ uint32_t lds[ONE_BLOCK / 64];
   uint32_t carry = 0;
-  for (size_t b0 = 0; b0 < n; b0 += (size_t)1024 * SCAN_ITEMS) {
+  for (size_t b0 = 0; b0 < n; b0 += (size_t)ONE_BLOCK * SCAN_ITEMS) {
     const size_t base = b0 + (size_t)threadIdx.x * SCAN_ITEMS;
     uint32_t x[SCAN_ITEMS];
 #pragma unroll
@@ -749,7 +735,7 @@ __global__ void __launch_bounds__(1024) k_scan_single(const uint32_t *__restrict
       s += v;
     }
     uint32_t tot;
-    const uint32_t off = carry + block_excl_scan<1024>(s, lds, tot);
+    const uint32_t off = carry + block_excl_scan<ONE_BLOCK>(s, lds, tot);
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++)
       if (base + k < n) out[base + k] = off + x[k];
@@ -761,14 +747,14 @@ __global__ void __launch_bounds__(1024) k_scan_single(const uint32_t *__restrict
 // the tiles per segment (and mbase: of the tiles of segments with >= 2 of them), computed straight
 // from the segment starts -- k_bs_tiles + one or two scans were 3-4 launches of ~5-17 us.  pub
 // (the last pass): the two totals and the entry count go to the lane's host buffer with a flag.
-__global__ void __launch_bounds__(1024) k_bs_geom(const uint32_t *__restrict__ seg, size_t S, uint32_t tile,
+__global__ void __launch_bounds__(ONE_BLOCK) k_bs_geom(const uint32_t *__restrict__ seg, size_t S, uint32_t tile,
                                                   uint32_t *__restrict__ tbase, uint32_t *__restrict__ mbase,
                                                   const uint32_t *__restrict__ valid, uint32_t *pub, uint32_t *flag,
                                                   uint32_t seq) {
-  __shared__ uint32_t lds[1024 / 64], lds2[1024 / 64];
+  __shared__ uint32_t lds[ONE_BLOCK / 64], lds2[ONE_BLOCK / 64];
   const size_t n = S + 1;
   uint32_t ct = 0, cm = 0;
-  for (size_t b0 = 0; b0 < n; b0 += (size_t)1024 * SCAN_ITEMS) {
+  for (size_t b0 = 0; b0 < n; b0 += (size_t)ONE_BLOCK * SCAN_ITEMS) {
     const size_t base = b0 + (size_t)threadIdx.x * SCAN_ITEMS;
     uint32_t xt[SCAN_ITEMS], xm[SCAN_ITEMS], st = 0, sm = 0;
 #pragma unroll
@@ -781,8 +767,8 @@ __global__ void __launch_bounds__(1024) k_bs_geom(const uint32_t *__restrict__ s
       sm += t > 1 ? t : 0u;
     }
     uint32_t tot_t, tot_m = 0;
-    const uint32_t off_t = ct + block_excl_scan<1024>(st, lds, tot_t);
-    const uint32_t off_m = mbase ? cm + block_excl_scan<1024>(sm, lds2, tot_m) : 0u;
+    const uint32_t off_t = ct + block_excl_scan<ONE_BLOCK>(st, lds, tot_t);
+    const uint32_t off_m = mbase ? cm + block_excl_scan<ONE_BLOCK>(sm, lds2, tot_m) : 0u;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++)
       if (base + k < n) {
@@ -812,37 +798,17 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint
     return;
   }
   if (n <= SCAN_SMALL) {
-    k_scan_single<<<1, 1024, 0, st>>>(in, n, out);
+    k_scan_single<<<1, ONE_BLOCK, 0, st>>>(in, n, out);
     TNS_LAUNCH_CHECK();
     return;
   }
   uint32_t *part = (uint32_t *)tmp.ensure(sizeof(uint32_t) * tiles);
   k_scan_reduce<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, n, part);
   TNS_LAUNCH_CHECK();
-  k_scan_parts<<<1, 1024, 0, st>>>(part, tiles);
+  k_scan_parts<<<1, ONE_BLOCK, 0, st>>>(part, tiles);
   TNS_LAUNCH_CHECK();
   k_scan_apply<<<(unsigned)tiles, SCAN_THREADS, 0, st>>>(in, n, part, out);
   TNS_LAUNCH_CHECK();
-}
-
-// tile size of pass p (0-based; 8192 or 4096 entries).  TNS_BS_TILES="t0,t1,t2" overrides
-// (tuning); passes beyond the list use its last entry.
-// 0 = automatic: 8192, except a last pass whose segments average <= 3584 entries (4096: the
-// one-tile segments fill it, and half the LDS doubles the blocks per CU -- pass 3 of a 2^24
-// opening MSM 1.02 -> 0.61 ms, profiles/r02_ab_sort_tiles.txt).
-static int pass_tile(int p) {
-  int t[8] = {0}, nt = 1;  // t[0] = 0: automatic (read per sort: tests switch it in-process)
-  if (const char *e = getenv("TNS_BS_TILES")) {
-    int k = 0;
-    for (const char *q = e; *q && k < 8;) {
-      const int v = atoi(q);
-      t[k++] = v == 4096 ? 4096 : v == 0 ? 0 : BS_TILE;
-      while (*q && *q != ',') q++;
-      if (*q == ',') q++;
-    }
-    if (k) nt = k;
-  }
-  return t[p < nt ? p : nt - 1];
 }
 
 // Groups the W*n digit entries of `scalars` by bucket (bucket_bits bits of bucket index;
@@ -864,9 +830,7 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   const size_t E = (size_t)W * n;
   if (E >= ((size_t)1 << 32)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one bucket sort");
   if (W > BS_TILE) throw Error(TNS_ERR_COMMITMENT, "too many MSM windows");
-  const bool corun = J.corun;  // the caller's choice survives the reset
   J = BucketSortJob();
-  J.corun = corun;
   J.ln = &ln;
   J.valid = valid;
   J.E = E;
@@ -887,81 +851,38 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   // remaining bits evenly (25-bit keys: 8, 8, 9 -- pass 2 with 256 instead of 512 bins writes
   // 128-byte runs: 1.21 -> 1.02 ms at 2^24)
   bits[npass - 1] = std::min(keybits, BS_MAXBITS);
-  // packed tail: the last pass keeps L <= 31 - ibits key bits so that its input fits one word
-  // (2^24 points: 7; 25-bit keys then split 9, 9, 7); TNS_BS_PACK=0 keeps keys + values (A/B)
+  // packed tail: the second-to-last pass writes (last-pass key bits, sign, point index) as one
+  // word when they fit (n <= 2^22 with a 9-bit last pass).  (A 7-bit last pass for 2^24 points,
+  // 9, 9, 7, measured slower: it moved the cost into 512-bin passes, +3.3 ms of sort per C4 step
+  // against -0.8 ms of reads.)  Values-only last pass (vo): whenever there is more than one pass --
+  // the accumulation reads no keys (C4: k_accumulate 9.10 -> 8.8 ms).
   int ibits = 1;
   while (((size_t)1 << ibits) < n) ibits++;
-  // (a 7-bit last pass for 2^24 points measured slower: 9, 9, 7 moved the cost into 512-bin
-  // passes, +3.3 ms of sort per C4 step against -0.8 ms of reads; so only when the usual split
-  // leaves room: n <= 2^22 with a 9-bit last pass).  Values-only last pass (vo): whenever there
-  // is more than one pass -- the accumulation reads no keys (C4: k_accumulate 9.10 -> 8.8 ms).
-  const char *pke = getenv("TNS_BS_PACK"), *voe = getenv("TNS_BS_VO");
-  J.vo = npass >= 2 && !(voe && voe[0] == '0');
+  J.vo = npass >= 2;
   // (unpack_value reads the window index from the low wb bits of the last pass's L key bits: L >= wb)
-  J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 && bits[npass - 1] >= J.wb;
+  J.pk = J.vo && npass >= 3 && bits[npass - 1] + ibits + 1 <= 32 && bits[npass - 1] >= J.wb;
   for (int p = 0, rest = keybits - bits[npass - 1]; p < npass - 1; p++) {
     bits[p] = (rest + (npass - 2 - p)) / (npass - 1 - p);
     rest -= bits[p];
-  }
-  const char *bbe = getenv("TNS_BS_BITS");
-  if (bbe && !strcmp(bbe, "last+1")) {  // (tests) one bit moved from the first pass to the last
-    if (npass >= 2 && bits[npass - 1] < BS_LASTBITS && bits[0] >= 2) {
-      bits[0]--;
-      bits[npass - 1]++;
-      J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 &&
-             bits[npass - 1] >= J.wb;
-    }
-  } else if (const char *e = bbe) {  // tuning: "b0,b1,..." (each <= 9, the last <= 10, summing to keybits)
-    int v[8], k = 0, sum = 0;
-    for (const char *q = e; *q && k < 8;) {
-      v[k] = atoi(q);
-      sum += v[k++];
-      while (*q && *q != ',') q++;
-      if (*q == ',') q++;
-    }
-    bool ok = k == npass && sum == keybits;
-    for (int p = 0; p < k; p++) ok = ok && v[p] >= 1 && v[p] <= (p == k - 1 && k > 1 ? BS_LASTBITS : BS_MAXBITS);
-    if (ok)
-      for (int p = 0; p < npass; p++) bits[p] = v[p];
-    if (ok)
-      J.pk = J.vo && npass >= 3 && !(pke && pke[0] == '0') && bits[npass - 1] + ibits + 1 <= 32 &&
-             bits[npass - 1] >= J.wb;
   }
   J.ibits = ibits;
   J.shared = shared;
   J.stride = stride;
   // key formats between passes: 2-byte keys into the last pass (its <= 9 key bits; C4 openings:
-  // pass 2 -> 3, sort kernels -0.6 ms per step, profiles/r03_ab_sort_k16.txt).  TNS_BS_K16=2
-  // also shrinks the earlier passes' keys (17 bits left after pass 1: one of them in the value's
-  // bit 30, free when the values stay below 2^30) -- measured SLOWER (pass 1 +0.2 ms, pass 2
-  // +0.35 ms per opening: half-dword stores of ~64-byte runs), so A/B only; =0: 4-byte keys.
-  const char *k16e = getenv("TNS_BS_K16");
-  const bool k16 = J.vo && !(k16e && k16e[0] == '0');  // (keys + values out: full keys)
-  const bool bit30 = (shared ? (uint64_t)(W - 1) * stride + n : (uint64_t)n) <= ((uint64_t)1 << 30);
-  const bool kall = k16e && k16e[0] == '2';  // every pass (A/B)
+  // pass 2 -> 3, sort kernels -0.6 ms per step, profiles/r03_ab_sort_k16.txt), 4-byte keys elsewhere
   for (int p = 0, rest = keybits; p < npass - 1; p++) {
     rest -= bits[p];
-    J.kf[p] = !k16 || (!kall && p != npass - 2) ? KF_U32
-              : rest <= 16                      ? KF_U16
-              : rest == 17 && bit30 && rest - bits[p + 1] >= 1 ? KF_U16S
-                                                               : KF_U32;
+    J.kf[p] = J.vo && p == npass - 2 && rest <= 16 ? KF_U16 : KF_U32;
   }
   if (J.pk) J.kf[npass - 2] = KF_U32;  // the packed words (pack_entry) are 4-byte
   int shift = keybits - bits[0];
 
-  // pass 1: scalars -> bins of the top bits[0] key bits
-  const bool runtime_pass1 = getenv("TNS_BS_RUNTIME_PASS1") != nullptr;  // (A/B: the runtime-plan kernels)
-  if (J.corun) {  // the small-register co-run kernels exist only as compile-time plans
-    bool have = false;
-    if (!runtime_pass1)
-      for (const Pass1Plan &p : kPass1Plans) have |= p.corun && p.tile == BS_CORUN_TILE && p.c == c && p.W == W;
-    if (!have) J.corun = false;  // full-size kernels instead (same result, no co-residence)
-  }
-  const int tile1 = J.corun ? BS_CORUN_TILE : W <= 4096 && pass_tile(0) ? pass_tile(0) : BS_TILE;
+  // pass 1: scalars -> bins of the top bits[0] key bits (a compile-time plan's kernels when there
+  // is one for this window plan, else the runtime-plan kernels)
+  const int tile1 = BS_TILE;
   const Pass1Plan *ct = nullptr;
-  if (!runtime_pass1)
-    for (const Pass1Plan &p : kPass1Plans)
-      if (p.tile == tile1 && p.c == c && p.W == W && p.corun == J.corun) ct = &p;
+  for (const Pass1Plan &p : kPass1Plans)
+    if (p.tile == tile1 && p.c == c && p.W == W) ct = &p;
   if ((size_t)tile1 < (size_t)W) throw Error(TNS_ERR_INVALID_PARAMETERS, "bucket sort: more windows than a pass-1 tile holds");
   A.spb = (size_t)tile1 / W;
   if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
@@ -971,9 +892,9 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   uint32_t **seg = J.seg;
   seg[0] = (uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1));
   seg[1] = (uint32_t *)ln.ws[11].ensure(sizeof(uint32_t) * (max_seg + 1));
-  const size_t tmin = J.corun ? BS_CORUN_TILE : 4096;  // the smallest pass tile
+  const size_t tmin = 4096;  // the smallest pass tile
   const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> bits[npass - 1]) + 1;
-  const size_t cnt_len = std::max((size_t)nb * T1, (size_t)(1u << bits[npass - 1] > BS_MAXBINS ? BS_LASTBINS : BS_MAXBINS) * max_tiles) + 1;
+  const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
@@ -982,8 +903,6 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
   const int kf1 = npass > 1 ? J.kf[0] : KF_U32;
   if (ct) ct->scatter<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
-  else if (tile1 == 4096)
-    k_bs_scatter1<4096><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
   else k_bs_scatter1<BS_TILE><<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
   TNS_LAUNCH_CHECK();
   k_bs_segs1<<<1, 256, 0, st>>>(offs, nb, T1, seg[0], valid);
@@ -1012,31 +931,24 @@ void bucket_sort_passes(BucketSortJob &J) {
     J.p = p;
     J.nb = 1 << bits[p];
     J.shift -= bits[p];
-    int tile = J.corun ? BS_CORUN_TILE : pass_tile(p);
-    if (!tile) tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
-    if (bits[p] > BS_MAXBITS) tile = BS_TILE;  // (the 1024-bin kernels: 8192-entry tiles only)
+    // 8192-entry tiles, except a last pass whose segments average <= 3584 entries (4096: the
+    // one-tile segments fill it, and half the LDS doubles the blocks per CU -- pass 3 of a 2^24
+    // opening MSM 1.02 -> 0.61 ms, profiles/r02_ab_sort_tiles.txt)
+    const int tile = (p == npass - 1 && (E >> (keybits - bits[p])) <= 3584) ? 4096 : BS_TILE;
     J.tile = tile;
     // In the last pass most segments fit one tile and rank locally; only segments of >= 2
     // tiles need the histogram pass and the global scan, so their counts get a compact layout,
     // sized from a readback of the tile totals (the top window's narrow digits make the
     // low-magnitude buckets' segments multi-tile).  All one-tile: no geometry at all (at 2^24
     // the full layout's histograms and scan over 512 bins x every tile took 0.34 ms).
-    J.last = p == npass - 1 && !getenv("TNS_BS_NO_LOCAL_LAST");
-    const char *ge = getenv("TNS_BS_GEOM");  // =0: k_bs_tiles + scans (A/B, a parity variant)
-    const bool geom1 = !(ge && ge[0] == '0');
-    if (geom1 && J.S + 1 <= SCAN_SMALL) {
+    J.last = p == npass - 1;
+    if (J.S + 1 <= SCAN_SMALL) {  // the tile geometry in one launch (k_bs_geom)
       uint32_t *pub = nullptr, *flag = nullptr, seq = 0;
-      if (J.last && !lane_sync_readback()) lane_publish_slot(ln, LANE_SLOT_SORT, &pub, &flag, &seq);
-      k_bs_geom<<<1, 1024, 0, st>>>(seg[J.cur], J.S, (uint32_t)tile, J.tbase, J.last ? J.mbase : nullptr, J.valid,
+      if (J.last) lane_publish_slot(ln, LANE_SLOT_SORT, &pub, &flag, &seq);
+      k_bs_geom<<<1, ONE_BLOCK, 0, st>>>(seg[J.cur], J.S, (uint32_t)tile, J.tbase, J.last ? J.mbase : nullptr, J.valid,
                                     pub, flag, seq);
       TNS_LAUNCH_CHECK();
       if (J.last) {
-        if (lane_sync_readback()) {
-          uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
-          TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-          TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-          TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        }
         J.pending = true;
         return;
       }
@@ -1050,16 +962,9 @@ void bucket_sort_passes(BucketSortJob &J) {
     if (J.last) {  // the readback; pass_rest runs after bucket_sort_finish's wait
       exclusive_scan(st, ln.ws[9], J.mcount, J.mbase, J.S + 1);
       // (with the entry count k_bs_segs1 wrote: the accumulation sizes its chunks from it)
-      if (lane_sync_readback()) {
-        uint32_t *h = (uint32_t *)ln.host2.ensure(3 * sizeof(uint32_t));
-        TNS_HIP(hipMemcpyAsync(h, J.tbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TNS_HIP(hipMemcpyAsync(h + 1, J.mbase + J.S, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        TNS_HIP(hipMemcpyAsync(h + 2, J.valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      } else {
-        const void *src[3] = {J.tbase + J.S, J.mbase + J.S, J.valid};
-        const size_t by[3] = {4, 4, 4};
-        lane_publish(ln, LANE_SLOT_SORT, 3, src, by);
-      }
+      const void *src[3] = {J.tbase + J.S, J.mbase + J.S, J.valid};
+      const size_t by[3] = {4, 4, 4};
+      lane_publish(ln, LANE_SLOT_SORT, 3, src, by);
       J.pending = true;
       return;
     }
@@ -1085,7 +990,7 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
     scan_len = (size_t)nb * h[1] + 1;
   }
   if (!ident) {
-    k_bs_desc<<<grid_for(S, 256), 256, 0, st>>>(J.tbase, S, J.desc);
+    k_bs_desc<<<grid_for(tiles_bound, 256, 4096), 256, 0, st>>>(J.tbase, S, J.desc);
     TNS_LAUNCH_CHECK();
   }
   // packed tail: pass npass - 2 writes packed words, the last pass bins them by their top bits
@@ -1097,25 +1002,13 @@ void bucket_sort_pass_rest(BucketSortJob &J, bool readback) {
   uint32_t *counts = J.counts, *offs = J.offs;
   if (!ident) {
     if (mb) TNS_HIP(hipMemsetAsync(counts + (scan_len - 1), 0, sizeof(uint32_t), st));  // the scan's total slot
-    if (nb > BS_MAXBINS)  // (a 10-bit last pass: 8192-entry tiles, 1024 bins)
-      k_bs_count<BS_TILE, BS_LASTBINS><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
-    else if (tile == BS_CORUN_TILE)
-      k_bs_count<BS_CORUN_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
-    else if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
+    if (tile == 4096) k_bs_count<4096><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     else k_bs_count<BS_TILE><<<(unsigned)tiles_bound, BS_BLOCK, 0, st>>>(G, S, tiles_bound, J.K[cur], counts);
     TNS_LAUNCH_CHECK();
     exclusive_scan(st, ln.ws[9], counts, offs, scan_len);
   }
   {
-    auto *kern = nb > BS_MAXBINS ? (pk == 0   ? k_bs_scatter<BS_TILE, 0, BS_LASTBINS>
-                                    : pk == 1 ? k_bs_scatter<BS_TILE, 1, BS_LASTBINS>
-                                    : pk == 2 ? k_bs_scatter<BS_TILE, 2, BS_LASTBINS>
-                                              : k_bs_scatter<BS_TILE, 3, BS_LASTBINS>)
-               : tile == BS_CORUN_TILE ? (pk == 0   ? k_bs_scatter<BS_CORUN_TILE, 0>
-                                          : pk == 1 ? k_bs_scatter<BS_CORUN_TILE, 1>
-                                          : pk == 2 ? k_bs_scatter<BS_CORUN_TILE, 2>
-                                                    : k_bs_scatter<BS_CORUN_TILE, 3>)
-               : tile == 4096 ? (pk == 0   ? k_bs_scatter<4096, 0>
+    auto *kern = tile == 4096 ? (pk == 0   ? k_bs_scatter<4096, 0>
                                  : pk == 1 ? k_bs_scatter<4096, 1>
                                  : pk == 2 ? k_bs_scatter<4096, 2>
                                            : k_bs_scatter<4096, 3>)
@@ -1137,12 +1030,7 @@ BucketOrder bucket_sort_finish(BucketSortJob &J) {
   MsmLane &ln = *J.ln;
   size_t entries = SIZE_MAX;  // unknown without the readback
   if (J.pending) {  // the last pass's tile totals
-    if (lane_sync_readback()) {
-      TNS_HIP(hipStreamSynchronize(ln.stream));
-      J.readback = ln.host2.p;
-    } else {
-      J.readback = lane_wait(ln, LANE_SLOT_SORT);
-    }
+    J.readback = lane_wait(ln, LANE_SLOT_SORT);
     J.pending = false;
     entries = ((const uint32_t *)J.readback)[2];
     bucket_sort_pass_rest(J, true);

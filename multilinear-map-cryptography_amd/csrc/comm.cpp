@@ -49,7 +49,18 @@ struct CallbackComm final : Comm {
 struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
   DevBuf send_b, recv_b;
+  // host staging owned by the communicator: the copies into and out of the collective's device
+  // buffers run asynchronously from pinned memory (no pageable copy that could block on the
+  // pending collective), and the caller's `recv` is written only once the stream has finished.
+  // After an abort the last D2H copy may still be queued: the staging buffer stays with the
+  // communicator, whose destructor waits for `done` before freeing it.
+  PinnedBuf send_h, recv_h;
+  hipEvent_t done = nullptr;
   ~RcclComm() override {
+    if (done) {
+      (void)hipEventSynchronize(done);
+      (void)hipEventDestroy(done);
+    }
     if (comm) (void)ncclCommDestroy(comm);
   }
   int kind() const override { return 2; }
@@ -62,15 +73,20 @@ struct RcclComm final : Comm {
   void allgather(Ctx *c, const void *send, size_t bytes, void *recv) override {
     if (!c) throw Error(TNS_ERR_INVALID_PARAMETERS, "the RCCL communicator needs a context");
     if (!comm) throw Error(TNS_ERR_DEVICE, "RCCL communicator was aborted by an earlier timeout");
-    void *ds = send_b.ensure(bytes ? bytes : 1), *dr = recv_b.ensure(bytes * size ? bytes * size : 1);
-    TNS_HIP(hipMemcpyAsync(ds, send, bytes, hipMemcpyHostToDevice, c->stream));
+    const size_t rb = bytes * size;
+    void *ds = send_b.ensure(bytes ? bytes : 1), *dr = recv_b.ensure(rb ? rb : 1);
+    void *hs = send_h.ensure(bytes ? bytes : 1), *hr = recv_h.ensure(rb ? rb : 1);
+    if (!done) TNS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    std::memcpy(hs, send, bytes);
+    TNS_HIP(hipMemcpyAsync(ds, hs, bytes, hipMemcpyHostToDevice, c->stream));
     TNS_NCCL(ncclAllGather(ds, dr, bytes, ncclUint8, comm, c->stream));
-    TNS_HIP(hipMemcpyAsync(recv, dr, bytes * size, hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipMemcpyAsync(hr, dr, rb, hipMemcpyDeviceToHost, c->stream));
+    TNS_HIP(hipEventRecord(done, c->stream));
     // wait with a deadline: a rank that never joins leaves the collective pending forever, so
-    // poll the stream (and RCCL's own async error) and abort the communicator past timeout_s
+    // poll the event (and RCCL's own async error) and abort the communicator past timeout_s
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spin = 0;; spin++) {
-      hipError_t q = hipStreamQuery(c->stream);
+      hipError_t q = hipEventQuery(done);
       if (q == hipSuccess) break;
       if (q != hipErrorNotReady) TNS_HIP(q);
       ncclResult_t ae = ncclSuccess;
@@ -88,6 +104,7 @@ struct RcclComm final : Comm {
       }
       if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+    std::memcpy(recv, hr, rb);
   }
 };
 
@@ -149,6 +166,8 @@ void Comm::exchange(Ctx *c, const void *send, size_t bytes, void *recv, const ch
   const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   total_s += el;
   if (el > max_s) max_s = el;
+  bytes_total += (double)bytes;
+  if ((double)bytes > bytes_max) bytes_max = (double)bytes;
 }
 
 // ---------------------------------------------------------------- combined exchanges

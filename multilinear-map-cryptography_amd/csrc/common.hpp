@@ -131,8 +131,6 @@ struct MsmLane {
   hipStream_t stream = nullptr;
   DevBuf ws[18];
   DevBuf fix;       // heavy-bucket level sums
-  PinnedBuf host;   // scalar bit length, then the per-set sums (TNS_MSM_SYNC_READBACK=1 path)
-  PinnedBuf host2;  // bucket sort: the largest last-pass segment (TNS_MSM_SYNC_READBACK=1 path)
   // the lane's host readbacks without a stream synchronize: a one-block kernel copies the words
   // into this fine-grained host buffer and then sets the slot's flag, which the host polls
   // (lane_publish / lane_wait, msm.hip).  Slots: 0 scalar bit length, 1 the sort's last-pass
@@ -148,7 +146,6 @@ void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const si
 const void *lane_wait(MsmLane &ln, int slot);
 // for kernels that publish themselves: the slot's data and flag (device views) and its new seq
 void lane_publish_slot(MsmLane &ln, int slot, uint32_t **data, uint32_t **flag, uint32_t *seq);
-bool lane_sync_readback();  // TNS_MSM_SYNC_READBACK=1: pinned copies + stream synchronize (A/B)
 
 // Per-level tables for exact interpolation on nodes {0..N-1} (interp.hip).
 struct InterpPlan {
@@ -230,7 +227,8 @@ struct KernelProfiler {
     for (auto &r : pending) {
       float ms = 0.f, t0 = 0.f, t1 = 0.f;
       if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
-        if (getenv("TNS_PROF_DEBUG")) fprintf(stderr, "prof %s %.3f ms\n", r.name.c_str(), ms);
+        static const bool dbg = getenv("TNS_PROF_DEBUG") != nullptr;  // (diagnostics: read once)
+        if (dbg) fprintf(stderr, "prof %s %.3f ms\n", r.name.c_str(), ms);
         auto &t = totals[r.name];
         t.ms += ms;
         t.launches += 1;
@@ -313,25 +311,8 @@ struct Ctx {
   std::map<std::tuple<size_t, size_t, size_t>, DevBuf *> bary_w;  // (N, first, count) -> weights
   bool lagrange_commit = true;           // prove via the Lagrange-basis SRS when available
   bool msm_tables = true;                // shared-bucket MSM on fixed bases with window tables
-  // two-lane MSM schedule (TNS_MSM_STAGGER=1): lane 1 (high-priority stream) starts its sort
-  // only once lane 0's sort is done, so it runs under lane 0's accumulation.  Off by default:
-  // the accumulation is issue-bound, a co-running sort slows it by as much as it hides
-  // (C4: 63.6 ms/step staggered, 62.6 not)
-  bool msm_stagger = false;
-  bool msm_serial = true;    // TNS_MSM_SERIAL=0: let the two lanes' accumulations run together
-  bool msm_cub_sort = false;  // TNS_MSM_SORT=cub: rocPRIM radix sort of a digit array (A/B)
-  // TNS_ACC_WAVES=k: k_accumulate as k resident 256-thread blocks per CU (grid-stride), leaving
-  // wave slots to a co-running sort; 0 (default) = one block per 256 chunks
-  int num_cu = 256, acc_waves = 0;
-  // sorted entries per k_accumulate thread (TNS_ACC_K fixes it; C4: 32 -> 62.0, 128 -> 61.1 ms).
-  // 0 = adaptive (msm.hip acc_chunk): the largest chunk <= 128 filling whole rounds of resident
-  // blocks; TNS_ACC_ROUNDS=0: the round-1 rule, 128 halved (down to 32) while the MSM would give
-  // fewer than acc_threads_cu threads per CU
-  int acc_k = 0, acc_threads_cu = 1024;
-  int red_l = 0;  // bucket-reduction group size (TNS_RED_L, power of two; 0 = 16)
-  int red_ch = 0;  // masked-sum chunk length (TNS_RED_CH, power of two; 0 = 16)
-  bool sc_tail = true;  // TNS_SC_TAIL=0: closure-free sum-check folds its last rounds launch by launch (A/B)
-  int msm_c = 0;   // TNS_MSM_C=c: per-window bucket width for the generic-base layout (A/B; 0 = cost model)
+  int num_cu = 256;
+  int upload_chunks = 4;  // drop-in provers: value-upload node ranges, each committed as it lands (tns_ctx_set_upload_chunks)
   KernelProfiler prof;
   ~Ctx();
 };
@@ -577,10 +558,6 @@ struct BucketSortJob {
   // bits, the sign and the point index i (ibits bits) -- and the last pass reads that word and
   // writes the accumulation's values only (no keys: runs come from the bucket starts)
   bool pk = false, vo = false, shared = false;  // vo: the last pass writes values only
-  // set before bucket_sort_begin: the sort runs beside another lane's accumulation, so it uses the
-  // small-register kernels (2048-entry pass tiles, one scalar per pass-1 thread) that fit in the
-  // 80 registers per lane k_accumulate's three waves per SIMD leave free
-  bool corun = false;
   int ibits = 0, p = 0;
   uint32_t stride = 0;
   int kf[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // key format pass p writes (bucket_sort.hip KF_*)
@@ -641,6 +618,7 @@ struct Comm {
   double timeout_s = 600.0;
   uint64_t seq = 0;
   double total_s = 0.0, max_s = 0.0;
+  double bytes_total = 0.0, bytes_max = 0.0;  // this rank's bytes per exchange step
   virtual ~Comm() = default;
   // 0 = one rank (self), 1 = host callback, 2 = RCCL
   virtual int kind() const = 0;

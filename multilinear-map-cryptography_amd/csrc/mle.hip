@@ -302,7 +302,10 @@ __device__ __forceinline__ Fr sc_eval(const ScPoly &q, const Fr (&v)[K]) {
 struct ScResult {
   Fr sums[4];
   uint32_t flag;
-  uint32_t pad[7];
+  // set by a device waiter whose 5 s bound for the host's challenge expired (it then released the
+  // kernels behind it without sums): sc_wait reports that cause at once instead of a missing publish
+  uint32_t wait_expired;
+  uint32_t pad[6];
 };
 
 // A round's challenge handed to round kernels queued before it existed: the host writes r and then
@@ -321,7 +324,7 @@ struct ScRDev {
 };
 constexpr uint32_t SC_CANCEL = 0xFFFFFFFFu;
 
-__global__ void __launch_bounds__(64) k_sc_wait_r(ScChal *chal, uint32_t seq, ScRDev *rd) {
+__global__ void __launch_bounds__(64) k_sc_wait_r(ScChal *chal, uint32_t seq, ScRDev *rd, ScResult *res) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   uint32_t f;
@@ -330,6 +333,7 @@ __global__ void __launch_bounds__(64) k_sc_wait_r(ScChal *chal, uint32_t seq, Sc
   while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq && f != SC_CANCEL) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {  // 5 s: the host is gone or failed
       f = SC_CANCEL;
+      __hip_atomic_store(&res->wait_expired, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }
     __builtin_amdgcn_s_sleep(2);
@@ -556,12 +560,16 @@ struct ScPing {
   Fr *B[MAX_SC_TABLES], *C[MAX_SC_TABLES];
 };
 
-// block 0 thread 0: the host's challenge for `seq`, else false (cancel / 5 s)
-__device__ bool sc_poll_host(ScChal *chal, uint32_t seq, Fr &r) {
+// block 0 thread 0: the host's challenge for `seq`, else false (cancel / 5 s: res->wait_expired)
+__device__ bool sc_poll_host(ScChal *chal, uint32_t seq, Fr &r, ScResult *res) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
   uint32_t f;
   while ((f = __hip_atomic_load(&chal->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != seq) {
-    if (f == SC_CANCEL || __builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) return false;
+    if (f == SC_CANCEL) return false;
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
+      __hip_atomic_store(&res->wait_expired, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (r itself is read with system-scope loads below)
@@ -587,7 +595,7 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
       bool ok = true;
       Fr r;
       if (blockIdx.x == 0) {
-        ok = sc_poll_host(chal, chal_base + rr, r);
+        ok = sc_poll_host(chal, chal_base + rr, r, res);
         if (ok) {
           sync->r[t] = r;
           __hip_atomic_store(&sync->rflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -740,14 +748,9 @@ __global__ void __launch_bounds__(256) k_sc_fold3(ScTables t, int k, size_t P, F
   }
 }
 
-static bool sc_fold3_on() {
-  const char *f3 = getenv("TNS_SC_FOLD3");  // =0: one launch per round (A/B)
-  return !(f3 && f3[0] == '0');
-}
-
 static unsigned sc_tail_round(unsigned nv) { return std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG)); }
 
-bool sumcheck_folds_take_flag_bytes(unsigned nv) { return sc_fold3_on() && sc_tail_round(nv) > 3; }
+bool sumcheck_folds_take_flag_bytes(unsigned nv) { return sc_tail_round(nv) > 3; }
 
 void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k, unsigned nv, const Fr *chal_pinned,
                                Fr *d_out, const uint8_t *flags, size_t n_flags) {
@@ -776,7 +779,6 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
   }
   Fr ch[64];
   std::memcpy(ch, chal_pinned, sizeof(Fr) * std::min(nv, 64u));
-  const bool fold3 = sc_fold3_on();
   bool first = true;
   for (unsigned rnd = 1; rnd < tail_rnd;) {
     ScTables tt{};
@@ -784,7 +786,7 @@ void sumcheck_zero_folds_async(Ctx *c, hipStream_t st, Fr *const *tables, int k,
       tt.in[i] = src[i];
       tt.out[i] = dst[i];
     }
-    if (fold3 && rnd + 2 < tail_rnd) {  // rounds rnd .. rnd + 2 in one pass
+    if (rnd + 2 < tail_rnd) {  // rounds rnd .. rnd + 2 in one pass (one read of the tables per three rounds)
       const size_t P = n >> (rnd + 2);
       TNS_PROF_ON(c, st, "sumcheck_round", 288.0 * (double)P * k);
       k_sc_fold3<<<grid_for(P, 256, 4096), 256, 0, st>>>(tt, k, P, ch[rnd - 1], ch[rnd], ch[rnd + 1],
@@ -828,6 +830,11 @@ static const ScResult &sc_wait(Ctx *c, uint32_t seq) {
   volatile ScResult *res = (volatile ScResult *)c->sc_mapped.p;
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 0; __atomic_load_n(&res->flag, __ATOMIC_ACQUIRE) != seq; spin++) {
+    if (const uint32_t w = __atomic_load_n(&res->wait_expired, __ATOMIC_RELAXED)) {
+      res->wait_expired = 0;
+      throw Error(TNS_ERR_DEVICE, "sum-check: a device waiter gave up on challenge #" + std::to_string(w) +
+                                      " after 5 s (the host's turn was too slow); its round did not run");
+    }
     if ((spin & 1023) == 1023 &&
         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 30.0) {
       TNS_HIP(hipStreamSynchronize(c->stream));
@@ -870,6 +877,7 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
   // zero once per sum-check (each round's last workgroup leaves it zero for the next round)
   TNS_HIP(hipMemsetAsync(R.counter, 0, sizeof(unsigned), c->stream));
   c->sc_mapped.ensure(sizeof(ScResult));
+  ((volatile ScResult *)c->sc_mapped.p)->wait_expired = 0;  // (nothing of an earlier call is still running)
   R.res_dev = (ScResult *)c->sc_mapped.dev;
   R.chal = (ScChal *)c->sc_handoff.ensure(sizeof(ScChal));
   R.chal_dev = (ScChal *)c->sc_handoff.dev;
@@ -878,11 +886,13 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
   return R;
 }
 
-// an integer sum-check knob from the environment (A/B and tests), else the default
-static int sc_env(const char *name, int dflt) {
-  const char *e = getenv(name);
-  return e && *e ? atoi(e) : dflt;
-}
+// The generic sum-check's schedule (round 5, profiles/r05_ab_sumcheck.txt):
+//  * rounds of <= 2^SC_SPLIT_LOG pairs run four lanes a pair (k_sc_round_split; 2^12-2^14 measured
+//    alike, at 2^16 the pairs-per-lane kernel is 2x faster);
+//  * the rounds of <= 2^SC_PTAIL_LOG pairs and the final fold run as one persistent launch of at
+//    most SC_PTAIL_BLOCKS one-wave blocks (k_sc_tail; 64 beat 16-1024);
+//  * each round's kernels are queued before its challenge exists (k_sc_wait_r).
+constexpr unsigned SC_SPLIT_LOG = 13, SC_PTAIL_LOG = 13, SC_PTAIL_BLOCKS = 64;
 
 // one round's launch (tables already in kernel order); returns the flag value to wait for
 template <bool FOLD, bool SKIP1>
@@ -892,9 +902,7 @@ static uint32_t sc_launch(ScRun &R, const ScTables &tt, size_t P) {
   // workgroups, each thread looping over pairs
   const uint32_t seq = ++R.c->sc_seq;
   hipStream_t st = R.c->stream;
-  // (TNS_SC_SPLIT_LOG: A/B of the split kernel's range; the sum-check knobs are read per call, so
-  // a test can set them in-process)
-  const size_t split_max = (size_t)1 << sc_env("TNS_SC_SPLIT_LOG", 13);
+  const size_t split_max = (size_t)1 << SC_SPLIT_LOG;
   if (P <= split_max) {  // four lanes a pair, 16 pairs a one-wave block (2^12-2^14 measured alike;
                          // at 2^16 the pairs-per-lane kernel is 2x faster)
     const unsigned g = grid_for(P, 16, R.max_grid * 4);
@@ -964,11 +972,10 @@ Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Sumc
 // case).  Round rr + 1's kernels are queued while round rr runs -- k_sc_wait_r, then the round
 // kernel -- so the host's part of a round (read the sums, interpolate, transcript, challenge) is
 // the only gap between two round kernels: the kernel launch latency (~15 us a round) leaves the
-// critical path.  TNS_SC_PREQUEUE=0 queues each round after its challenge exists (A/B).
+// critical path.
 static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &claimed,
                                  const SumcheckTerm *terms, int n_terms, HostTranscript &tr, Fr *rounds,
                                  Fr *challenges, Fr *final_vals, Fr *final_eval) {
-  const bool prequeue = sc_env("TNS_SC_PREQUEUE", 1) != 0;
   const size_t n = (size_t)1 << nv;
   Fr *bufB[MAX_SC_TABLES], *bufC[MAX_SC_TABLES];
   for (int i = 0; i < k; i++) {
@@ -985,15 +992,13 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
   const uint32_t chal_base = c->sc_chal_seq;
   c->sc_chal_seq += nv + 1;
   R.chal->flag = 0;  // (no stale value can match: chal_base + i is fresh)
-  // the persistent tail (k_sc_tail) from the first round r0 >= 2 of <= 2^tail_log pairs
-  const unsigned tail_log = (unsigned)sc_env("TNS_SC_TAIL_LOG", 13);  // its range (0: no tail kernel, A/B)
+  // the persistent tail (k_sc_tail) from the first round r0 >= 2 of <= 2^SC_PTAIL_LOG pairs
   unsigned r0 = nv;
-  if (tail_log > 0)
-    for (unsigned rr = 2; rr < nv; rr++)
-      if ((n >> (rr + 1)) <= ((size_t)1 << tail_log)) {
-        r0 = rr;
-        break;
-      }
+  for (unsigned rr = 2; rr < nv; rr++)
+    if ((n >> (rr + 1)) <= ((size_t)1 << SC_PTAIL_LOG)) {
+      r0 = rr;
+      break;
+    }
   const bool tail = r0 < nv;
   uint32_t tail_seq = 0;
   // queue round rr (rr >= 1: behind the wait for challenge r_{rr-1}); rr == nv: the final fold
@@ -1009,9 +1014,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
         }
         tail_seq = c->sc_seq + 1;
         c->sc_seq += nv - r0 + 1;
-        // TNS_SC_TAIL_BLOCKS: the tail's one-wave blocks at most (A/B; 16 / 32 / 64 / 256 / 1024 measured)
-        const size_t gmax = (size_t)std::max(1, sc_env("TNS_SC_TAIL_BLOCKS", 64));
-        const unsigned g = (unsigned)std::min<size_t>(gmax, std::max<size_t>(1, (n >> (r0 + 1)) / 16));
+        const unsigned g = (unsigned)std::min<size_t>(SC_PTAIL_BLOCKS, std::max<size_t>(1, (n >> (r0 + 1)) / 16));
 #define TNS_SC_K(K)                                                                                             \
   k_sc_tail<K><<<g, 64, 0, c->stream>>>(pp, R.q_dev, r0, nv, n, R.chal_dev, chal_base, R.res_dev, tail_seq, \
                                        R.partials, R.counter, sync)
@@ -1027,7 +1030,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       return tail_seq + (rr - r0);
     }
     if (rr > 0) {
-      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, chal_base + rr, R.rd);
+      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, chal_base + rr, R.rd, R.res_dev);
       TNS_LAUNCH_CHECK();
     }
     ScTables tt{};
@@ -1056,7 +1059,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     char lab[64];
     uint32_t seq = queue(0);  // (nv == 0: the final kernel, reading the tables as they are)
     for (unsigned rnd = 0; rnd < nv; rnd++) {
-      const uint32_t seq_next = prequeue ? queue(rnd + 1) : 0;
+      const uint32_t seq_next = queue(rnd + 1);
       Fr e[4];
       sc_round_sums(R, seq, e);
       if (rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
@@ -1075,7 +1078,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       if (challenges) challenges[rnd] = ch;
       cur = horner_host(coeffs, 4, ch);
       publish(rnd, ch);
-      seq = prequeue ? seq_next : queue(rnd + 1);
+      seq = seq_next;
     }
     const ScResult &res = sc_wait(c, seq);
     Fr vals[MAX_SC_TABLES];
@@ -1127,7 +1130,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
   // closure-free chains hand their last folds to k_sc_fold_tail: from round `tail_rnd` on
   // (input tables of n >> (tail_rnd - 1) <= 2^SC_TAIL_LOG entries) only the transcript runs
   const unsigned tail_rnd =
-      (c->sc_tail && !has_terms && k > 0 && nv >= 2) ? std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG)) : nv + 1;
+      (!has_terms && k > 0 && nv >= 2) ? std::max(1u, nv + 1 - std::min(nv, SC_TAIL_LOG)) : nv + 1;
   Fr tail_ch[64];
   for (unsigned rnd = 0; rnd < nv; rnd++) {
     const size_t P = n >> (rnd + 1);  // output pairs of this round
@@ -1211,7 +1214,7 @@ int sumcheck_prove_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const Fr &
     if (nv > 0) {  // (the challenge to device memory: k_sc_final reads it there)
       R.chal->r = r_prev;
       __atomic_store_n(&R.chal->flag, ++c->sc_chal_seq, __ATOMIC_RELEASE);
-      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, c->sc_chal_seq, R.rd);
+      k_sc_wait_r<<<1, 64, 0, c->stream>>>(R.chal_dev, c->sc_chal_seq, R.rd, R.res_dev);
       TNS_LAUNCH_CHECK();
     }
     k_sc_final<<<1, 64, 0, c->stream>>>(tt, k, R.rd, nv > 0, R.res_dev, seq);

@@ -15,12 +15,9 @@
 // Pipeline (per MSM lane stream):
 //  0. k_scalar_bits: bit length of the largest scalar -> windows above it are skipped
 //     (trace commitments -- addresses, small values, flags -- are narrow).
-//  1.-3. the bucket order (bucket_sort.hip, the default): the signed c-bit digits are computed
-//     inside the first pass of a hand-written MSD counting sort (no digit array, zero digits never
-//     enter it); its last pass writes the point indices | sign<<31 alone and the bucket starts.
-//     TNS_MSM_SORT=cub (A/B) instead runs k_digits (key = bucket, sentinel for zero digits),
-//     hipCUB's radix sort of the (key, value) pairs and k_bucket_bounds -- the only use of the
-//     hipcub include below.
+//  1.-3. the bucket order (bucket_sort.hip): the signed c-bit digits are computed inside the
+//     first pass of a hand-written MSD counting sort (no digit array, zero digits never enter it);
+//     its last pass writes the point indices | sign<<31 alone and the bucket starts.
 //  4. k_accumulate: load-balanced -- each thread owns acc_k consecutive sorted entries
 //     and XYZZ-madds the (possibly negated) affine points run by run; runs that cross a
 //     chunk boundary leave a head/tail partial; k_bucket_fixup completes those buckets (heavy buckets'
@@ -32,7 +29,6 @@
 //     (short dependency chains -- single-thread point-add chains are the slow part).
 //  6. host: per-window Horner (per-window layout) or nothing (shared layout).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>  // TNS_MSM_SORT=cub only (A/B against the hand-written sort)
 
 #include <algorithm>
 #include <chrono>
@@ -121,89 +117,8 @@ __global__ void __launch_bounds__(256) k_scalar_bits(const Fr *__restrict__ scal
   block_atomic_max2(b, 0u, bits, nullptr);
 }
 
-// shared = false: key = (w << (c-1)) | (|d| - 1), value = i | sign<<31
-// shared = true:  key = |d| - 1,                  value = (w * stride + i) | sign<<31
-// The scalars as the sort's digit pass reads them (SortInput): Montgomery forms, canonical forms
-// (the opening quotients) or raw u64 values (trace addresses, lookup indices; zero above n_u64).
-__global__ void __launch_bounds__(256) k_digits(SortInput in, size_t n, int c, int W,
-                                                uint32_t sentinel, bool shared, uint32_t stride,
-                                                uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
-       i += (size_t)gridDim.x * blockDim.x) {
-    Fr k = Fr::zero();
-    if (in.u64) {
-      const uint64_t x = i < in.n_u64 ? in.u64[i] : 0;
-      k.v[0] = (uint32_t)x;
-      k.v[1] = (uint32_t)(x >> 32);
-    } else {
-      k = in.mont ? from_mont(in.fr[i]) : in.fr[i];
-    }
-    uint32_t carry = 0;
-    const uint32_t half = 1u << (c - 1);
-    for (int w = 0; w < W; w++) {
-      int bit = w * c;
-      int limb = bit >> 5, sh = bit & 31;
-      uint64_t lo = limb < 8 ? k.v[limb] : 0;
-      uint64_t hi = limb + 1 < 8 ? k.v[limb + 1] : 0;
-      uint32_t raw = (uint32_t)(((lo | (hi << 32)) >> sh) & ((1u << c) - 1));
-      uint32_t val = raw + carry;
-      uint32_t neg = 0, mag;
-      if (val > half) {
-        mag = (1u << c) - val;
-        neg = 1;
-        carry = 1;
-      } else {
-        mag = val;
-        carry = 0;
-      }
-      uint32_t key = mag ? ((shared ? 0u : ((uint32_t)w << (c - 1))) | (mag - 1)) : sentinel;
-      keys[(size_t)w * n + i] = key;
-      vals[(size_t)w * n + i] = (uint32_t)(shared ? (size_t)w * stride + i : i) | (neg << 31);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(256) k_bucket_bounds(const uint32_t *__restrict__ keys, size_t total,
-                                                       uint32_t sentinel, uint32_t *__restrict__ start,
-                                                       uint32_t *__restrict__ end,
-                                                       uint32_t *__restrict__ valid) {
-  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < total;
-       p += (size_t)gridDim.x * blockDim.x) {
-    uint32_t k = keys[p];
-    if (k == sentinel) continue;
-    if (p == 0 || keys[p - 1] != k) start[k] = (uint32_t)p;
-    uint32_t nx = (p + 1 < total) ? keys[p + 1] : sentinel;
-    if (nx != k) end[k] = (uint32_t)(p + 1);
-    if (nx == sentinel) *valid = (uint32_t)(p + 1);
-  }
-}
-
-// A/B builds only (tools/build_variant.sh): -DTNS_ACC_PTMASK=0xffff gathers every point from a
-// 4 MB slice (L2-resident; wrong sums) to separate the gather's cost from the arithmetic's
-#ifndef TNS_ACC_PTMASK
-#define TNS_ACC_PTMASK 0x7fffffffu
-#endif
-
-// TNS_ACC_PREFETCH=1 (A/B build): software-pipelined gathers -- entry p + 1's point and entry
-// p + 2's value are loaded while entry p is added
-#ifndef TNS_ACC_PREFETCH
-#define TNS_ACC_PREFETCH 0
-#endif
-
-// the accumulation's point gather (TNS_ACC_NT=1 A/B build: non-temporal loads)
-typedef uint32_t acc_v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ G1Affine load_point(const G1Affine *__restrict__ pts, uint32_t i) {
-#if defined(TNS_ACC_NT) && TNS_ACC_NT
-  const acc_v4u *s = reinterpret_cast<const acc_v4u *>(pts + i);
-  G1Affine q;
-  acc_v4u *d = reinterpret_cast<acc_v4u *>(&q);
-#pragma unroll
-  for (int k = 0; k < 4; k++) d[k] = __builtin_nontemporal_load(s + k);
-  return q;
-#else
-  return pts[i];
-#endif
-}
+// the accumulation's point gather
+__device__ __forceinline__ G1Affine load_point(const G1Affine *__restrict__ pts, uint32_t i) { return pts[i]; }
 
 struct HeadTail {
   G1Xyzz head, tail;
@@ -221,25 +136,22 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ bstar
   return (uint32_t)lo;
 }
 
-// keys == nullptr (packed sort tail): a chunk finds its first bucket by a binary search of the
+// keys == nullptr (values-only sort tail): a chunk finds its first bucket by a binary search of the
 // bucket starts and every later run boundary from the next start -- no key per entry.
-// TNS_ACC_MINB (A/B builds): __launch_bounds__ minimum blocks per CU (4: 128 VGPRs, 4 waves/SIMD)
-#ifndef TNS_ACC_MINB
-#define TNS_ACC_MINB 1
-#endif
 // KEYS (a template parameter, so the default values-only sort's variant carries none of the key
 // path's registers): the sort left a key per entry (else the runs come from the bucket starts)
 template <bool KEYS>
-__global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t *__restrict__ keys,
+__global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__ keys,
                                                     const uint32_t *__restrict__ vals,
                                                     const uint32_t *__restrict__ valid_p,
                                                     const G1Affine *__restrict__ pts,
                                                     G1Xyzz *__restrict__ buckets,
                                                     HeadTail *__restrict__ ht, size_t nchunks, int ks,
                                                     int acc_k, const uint32_t *__restrict__ bstart, size_t nb,
-                                                    uint2 *__restrict__ cbk) {
+                                                    uint2 *__restrict__ cbk, uint32_t *__restrict__ spans) {
   // entry positions are 32-bit (a sort holds < 2^31 entries, msm_launch_sort): one VGPR each
   const uint32_t valid = *valid_p;
+  bool crossed = false;  // this thread left a head or tail partial (k_fix_level / k_bucket_fixup work)
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
     const uint32_t a = (uint32_t)t * (uint32_t)acc_k;
@@ -265,10 +177,6 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
     bool first = true;
     const uint32_t first_bucket = cur;
     G1Xyzz acc = G1Xyzz::inf();
-#if TNS_ACC_PREFETCH
-    uint32_t v1 = vals[a], v2 = a + 1 < b ? vals[a + 1] : 0u;
-    G1Affine q1 = load_point(pts, v1 & TNS_ACC_PTMASK);
-#endif
     for (uint32_t p = a;; p++) {
       const bool brk = KEYS ? p >= b || (keys[p] >> ks) != cur : p >= b || p >= nxt;
       if (brk) {  // flush the run of bucket `cur`
@@ -276,6 +184,7 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
         if (first && head_run) ht[t].head = acc;
         else if (p >= b && tail) ht[t].tail = acc;
         else buckets[cur] = acc;
+        crossed |= (first && head_run) || (p >= b && tail);
         if (p >= b) {
           cbk[t] = make_uint2(first_bucket, cur);  // the buckets of entries a and b - 1 (k_fix_level)
           break;
@@ -293,18 +202,8 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
       }
       // (gathering entry p + 1 ahead of this addition measured no faster: 39.48 vs 39.46 ms of
       // accumulation per C4 step -- three waves per SIMD hide the gather)
-#if TNS_ACC_PREFETCH
-      const uint32_t v = v1;
-      G1Affine q = q1;
-      if (p + 1 < b) {  // entry p + 1's point (its value arrived an iteration ago), entry p + 2's value
-        q1 = load_point(pts, v2 & TNS_ACC_PTMASK);
-        v1 = v2;
-        if (p + 2 < b) v2 = vals[p + 2];
-      }
-#else
       const uint32_t v = vals[p];
-      G1Affine q = load_point(pts, v & TNS_ACC_PTMASK);
-#endif
+      G1Affine q = load_point(pts, v & 0x7fffffffu);
       // -y = M - y (y canonical); the identity (0, 0) keeps y = 0
       const Fq ny = const_minus_dev<FqCfg, false>(q.y);
       const bool negy = (v >> 31) && !q.y.is_zero();
@@ -313,6 +212,9 @@ __global__ void __launch_bounds__(256, TNS_ACC_MINB) k_accumulate(const uint32_t
       acc = xyzz_madd_lazy(acc, q);
     }
   }
+  // one flag per MSM: no run crossed a chunk (the 22-bit address commitment at C4: every bucket's
+  // four entries inside one chunk) -> the fixup levels have nothing to do
+  if (__any(crossed) && (threadIdx.x & 63) == 0) atomicOr(spans, 1u);
 }
 
 // Heavy buckets (skewed scalars: repeated values, small ranges) span many chunks; their
@@ -332,12 +234,25 @@ struct FixLevels {
 // over those lanes (3 dependent additions instead of one thread's chain of 7: the narrow value
 // commitment's heavy buckets fill thousands of groups and this level ran at half a wave per SIMD)
 static_assert(FIX_FAN == 8, "k_fix_level's butterfly assumes 8 lanes per group");
-__global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ keys,
-                                                   const uint32_t *__restrict__ valid_p,
-                                                   const HeadTail *__restrict__ ht, const G1Xyzz *__restrict__ below,
-                                                   int level, size_t n_groups, G1Xyzz *__restrict__ out, int ks,
-                                                   int acc_k, const uint2 *__restrict__ cbk) {
-  const size_t valid = *valid_p;
+// one MSM's level-l groups (blockIdx.y picks the MSM: a pair's two tails run as one launch)
+struct FixLevelSet {
+  const uint32_t *valid;
+  const HeadTail *ht;
+  const G1Xyzz *below;
+  G1Xyzz *out;
+  const uint2 *cbk;
+  size_t n_groups;  // 0: this MSM has no level l
+  int acc_k;
+};
+struct FixLevelArgs {
+  FixLevelSet s[2];
+};
+__global__ void __launch_bounds__(256) k_fix_level(FixLevelArgs A, int level) {
+  const FixLevelSet &S = A.s[blockIdx.y];
+  const size_t n_groups = S.n_groups;
+  if (!n_groups || !S.valid[1]) return;  // (valid[1]: some run crossed a chunk, k_accumulate)
+  const size_t valid = *S.valid;
+  const int acc_k = S.acc_k;
   const int j = threadIdx.x & (FIX_FAN - 1);
   const size_t stride = (size_t)gridDim.x * blockDim.x / FIX_FAN;
   // group-uniform trip count (blockDim.x is a multiple of FIX_FAN): the 8 lanes of a group stay together
@@ -347,13 +262,13 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
     const size_t a = g * span, b = a + span;  // entries covered
     // every entry of [a, b) in one bucket: the bucket of entry a (that chunk's first) is the bucket
     // of entry b - 1 (the last chunk's last), as k_accumulate recorded them
-    const bool uniform = b <= valid && cbk[a / acc_k].x == cbk[(b - 1) / acc_k].y;
+    const bool uniform = b <= valid && S.cbk[a / acc_k].x == S.cbk[(b - 1) / acc_k].y;
     // a wave whose 8 groups all span several buckets has nothing to sum (those sums are never
     // read): skip its butterfly -- most of a narrow commitment's groups (the 22-bit address MSM:
-    // ~4 entries a bucket) are such, and the level ran 0.9 ms beside the value accumulation
+    // ~4 entries a bucket) are such
     if (!__any(uniform)) continue;
     G1Xyzz acc = G1Xyzz::inf();
-    if (uniform) acc = level == 1 ? ht[g * FIX_FAN + j].head : below[g * FIX_FAN + j];
+    if (uniform) acc = level == 1 ? S.ht[g * FIX_FAN + j].head : S.below[g * FIX_FAN + j];
     for (int off = FIX_FAN / 2; off > 0; off >>= 1) {  // every lane of the wave takes part
       G1Xyzz o;
       const uint32_t *pa = reinterpret_cast<const uint32_t *>(&acc);
@@ -362,7 +277,7 @@ __global__ void __launch_bounds__(256) k_fix_level(const uint32_t *__restrict__ 
       for (int q = 0; q < (int)(sizeof(G1Xyzz) / 4); q++) po[q] = __shfl_xor(pa[q], off);
       if (uniform) acc = xyzz_add_lazy(acc, o);
     }
-    if (uniform && j == 0) out[g] = acc;
+    if (uniform && j == 0) S.out[g] = acc;
   }
 }
 
@@ -422,11 +337,34 @@ __device__ __forceinline__ G1Xyzz wave_sum_xyzz(G1Xyzz acc) {
   return acc;
 }
 
-__global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict__ start,
-                                                      const uint32_t *__restrict__ end,
-                                                      const HeadTail *__restrict__ ht, FixLevels F,
-                                                      G1Xyzz *__restrict__ buckets, size_t nb, int acc_k, bool waves) {
+// one MSM's buckets (blockIdx.y picks the MSM: a pair's two tails run as one launch)
+struct FixupSet {
+  const uint32_t *start, *end;
+  const uint32_t *valid;  // [1]: some run crossed a chunk (else only the empty buckets need writing)
+  const HeadTail *ht;
+  FixLevels F;
+  G1Xyzz *buckets;
+  size_t nb;
+  int acc_k;
+};
+struct FixupArgs {
+  FixupSet s[2];
+};
+__global__ void __launch_bounds__(256) k_bucket_fixup(FixupArgs A) {
+  const FixupSet &S = A.s[blockIdx.y];
+  const uint32_t *__restrict__ start = S.start;
+  const uint32_t *__restrict__ end = S.end;
+  const HeadTail *__restrict__ ht = S.ht;
+  const FixLevels &F = S.F;
+  G1Xyzz *__restrict__ buckets = S.buckets;
+  const size_t nb = S.nb;
+  const int acc_k = S.acc_k;
   const int lane = threadIdx.x & 63;
+  if (!S.valid[1]) {  // every run inside one chunk: k_accumulate wrote every non-empty bucket
+    for (size_t bk = blockIdx.x * (size_t)blockDim.x + threadIdx.x; bk < nb; bk += (size_t)gridDim.x * blockDim.x)
+      if (start[bk] == end[bk]) buckets[bk] = G1Xyzz::inf();
+    return;
+  }
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   // wave-uniform trip count: a wave meets its lanes' heavy runs together
   for (size_t base = blockIdx.x * (size_t)blockDim.x + (threadIdx.x & ~63u); base < nb; base += stride) {
@@ -437,7 +375,7 @@ __global__ void __launch_bounds__(256) k_bucket_fixup(const uint32_t *__restrict
       e = end[bk];
     }
     const size_t tf = s / acc_k, tl = e > s ? (e - 1) / acc_k : tf;
-    const bool heavy = waves && bk < nb && tl - tf > FIX_WAVE_SPAN;
+    const bool heavy = bk < nb && tl - tf > FIX_WAVE_SPAN;
     // the wave's heavy runs, one at a time: lane j adds items j, j + 64, ..., then a butterfly
     for (uint64_t hm = __ballot(heavy); hm; hm &= hm - 1) {
       const int src = __ffsll((unsigned long long)hm) - 1;
@@ -642,10 +580,6 @@ __global__ void __launch_bounds__(256) k_dbl_times(G1Xyzz *__restrict__ x, size_
 
 // the window a table for n points uses: the shared-layout optimum for full-width scalars
 static int table_window(size_t n) {
-  if (const char *e = getenv("TNS_TABLE_C")) {  // tuning: force the table window
-    const int c = atoi(e);
-    if (c >= 4 && c <= 22) return c;
-  }
   // no near-tie preference for the shared tables: at 2^20 + 1 points c = 19 (W = 14) was taken
   // over c = 20 (W = 13, 2 % cheaper in plan_cost) and the 2^20 MSM over it ran 2.42 vs 2.01 ms
   // (deeper buckets: 56 vs 26 entries each, k_bucket_fixup 0.28 vs 0.07 ms)
@@ -736,6 +670,11 @@ struct MsmJob {
   uint32_t *keys2 = nullptr, *vals2 = nullptr, *bstart = nullptr, *bend = nullptr, *valid = nullptr;
   int ks = 0, acc_k = 0;
   size_t nchunks = 0, n = 0;
+  G1Xyzz *buckets = nullptr;  // set before the accumulation (a two-set tail: the pair's buckets adjoin)
+  // where msm_complete finds the per-set sums: the slot of res_lane (this lane, or the lane that ran
+  // a two-set tail), set res_set of res_sets
+  MsmLane *res_lane = nullptr;
+  int res_set = 0, res_sets = 1;
 };
 
 // ---------------------------------------------------------------- lane readbacks
@@ -756,11 +695,6 @@ __global__ void __launch_bounds__(256) k_lane_publish(PubArgs a, uint32_t *dst, 
   __threadfence_system();  // every thread's words reach host memory before the flag
   __syncthreads();
   if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-bool lane_sync_readback() {  // (read per call: the parity tests switch it in-process)
-  const char *e = getenv("TNS_MSM_SYNC_READBACK");
-  return e && e[0] == '1';
 }
 
 void lane_publish(MsmLane &ln, int slot, int n, const void *const *src, const size_t *bytes) {
@@ -813,42 +747,31 @@ const void *lane_wait(MsmLane &ln, int slot) {
 // the largest bit length of Montgomery scalars; the sort then reads them as they are
 // (SortInput::mont: canonicalised in its digit pass instead of through a canonical copy)
 static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
-  unsigned *d_bits = (unsigned *)ln.ws[4].ensure(sizeof(unsigned));
-  unsigned *h_bits = (unsigned *)ln.host.ensure(sizeof(unsigned));
+  unsigned *d_bits = (unsigned *)ln.ws[4].ensure(2 * sizeof(unsigned));  // (then the sort's two counters)
   TNS_HIP(hipMemsetAsync(d_bits, 0, sizeof(unsigned), ln.stream));
   k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, nullptr);
   TNS_LAUNCH_CHECK();
-  if (lane_sync_readback()) {
-    TNS_HIP(hipMemcpyAsync(h_bits, d_bits, sizeof(unsigned), hipMemcpyDeviceToHost, ln.stream));
-  } else {
-    const void *src[1] = {d_bits};
-    const size_t by[1] = {sizeof(unsigned)};
-    lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
-  }
+  const void *src[1] = {d_bits};
+  const size_t by[1] = {sizeof(unsigned)};
+  lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
   SortInput in;
   in.fr = scalars;
   in.mont = true;
   return in;
 }
 
-static unsigned bits_result(MsmLane &ln) {
-  if (!lane_sync_readback()) return *(const unsigned *)lane_wait(ln, LANE_SLOT_BITS);
-  TNS_HIP(hipStreamSynchronize(ln.stream));
-  return *(unsigned *)ln.host.p;
-}
+static unsigned bits_result(MsmLane &ln) { return *(const unsigned *)lane_wait(ln, LANE_SLOT_BITS); }
 
 // Entries per accumulation thread.  Per-window plans (the narrow commitments: runs of a few
 // entries, flush- and latency-bound): 128, halved down to 32 while the MSM gives fewer than
-// acc_threads_cu threads per CU -- short chunks shorten each thread's dependent chain.
+// ACC_THREADS_CU threads per CU -- short chunks shorten each thread's dependent chain.
 // Table-window plans (full-width scalars) whose count the sort read back: the largest chunk
 // <= 128 that fills whole rounds of the resident blocks (fewer chunks, fewer head/tail partials
 // for the fixup: C2 2.17 -> 2.11 ms; the 2^24 openings keep 128, `profiles/r02_ab_acc_rounds.txt`).
-// TNS_ACC_K forces a chunk; TNS_ACC_ROUNDS=0 / 1 forces the first / second rule.
+constexpr int ACC_THREADS_CU = 1024;
 static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
-  if (ctx->acc_k > 0) return ctx->acc_k;
-  const char *ar = getenv("TNS_ACC_ROUNDS");
-  if (ar ? ar[0] == '0' : !table_plan) {
-    const size_t want = (size_t)ctx->num_cu * ctx->acc_threads_cu;
+  if (!table_plan) {
+    const size_t want = (size_t)ctx->num_cu * ACC_THREADS_CU;
     int k = 128;
     while (k > 32 && entries / k < want) k /= 2;
     return k;
@@ -858,9 +781,7 @@ static int acc_chunk(Ctx *ctx, size_t entries, bool table_plan) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_accumulate<false>, 256, 0) != hipSuccess || b < 1) b = 3;
     return b;
   }();
-  const size_t slots = (size_t)ctx->num_cu * bpc * 256;
-  size_t kmax = 128;  // TNS_ACC_TABLE_KMAX: the chunk cap of this rule (A/B)
-  if (const char *e = getenv("TNS_ACC_TABLE_KMAX")) kmax = std::max(16, atoi(e));
+  const size_t slots = (size_t)ctx->num_cu * bpc * 256, kmax = 128;
   const size_t rounds = std::max<size_t>(1, (entries + kmax * slots - 1) / (kmax * slots));
   const size_t k = (entries + rounds * slots - 1) / (rounds * slots);
   return (int)std::max<size_t>(16, std::min<size_t>(kmax, k));
@@ -894,13 +815,9 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
     G1Xyzz *d = (G1Xyzz *)ln.ws[0].ensure(sizeof(G1Xyzz));
     k_msm_tiny<<<1, 64, 0, st>>>(points, scalars, (int)n, d);
     TNS_LAUNCH_CHECK();
-    if (lane_sync_readback()) {
-      TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(G1Xyzz)), d, sizeof(G1Xyzz), hipMemcpyDeviceToHost, st));
-    } else {
-      const void *src[1] = {d};
-      const size_t by[1] = {sizeof(G1Xyzz)};
-      lane_publish(ln, LANE_SLOT_SUMS, 1, src, by);
-    }
+    const void *src[1] = {d};
+    const size_t by[1] = {sizeof(G1Xyzz)};
+    lane_publish(ln, LANE_SLOT_SUMS, 1, src, by);
     J.tiny = true;
     record_now();
     return;
@@ -910,9 +827,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   // plan: per-window layout, or the shared layout when a fixed-base table covers the points
   MsmPlan &P = J.P;
   P = MsmPlan();
-  const char *w1 = getenv("TNS_MSM_W1");  // =0: no single-window plan (A/B, tests)
-  P.c = best_window(n, (int)bits, 20, false, w1 && w1[0] == '0' ? 0 : 23);
-  if (ctx->msm_c >= 4) P.c = ctx->msm_c;
+  P.c = best_window(n, (int)bits, 20, false, 23);
   P.W = windows_for((int)bits, P.c);
   if (fb && ctx->msm_tables && fb->n >= fb_off + n && (uint64_t)fb->n * fb->W < ((uint64_t)1 << 31)) {
     const int Ws = windows_for((int)bits, fb->c);
@@ -933,50 +848,12 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   J.acc_k = acc_k;
   J.nchunks = (total + acc_k - 1) / acc_k;
   J.n = n;
-  if (!ctx->msm_cub_sort) {
-    J.sort_prof.reset(new ProfScope(ctx->prof, st, "msm_sort", 32.0 * n + 16.0 * total));
-    J.valid = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t));
-    bucket_sort_begin(ln, in, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
-    J.sort_pending = true;
-    J.passes_pending = true;
-    if (!defer) msm_finish_sort(J);
-    return;
-  }
-  uint32_t *keys = (uint32_t *)ln.ws[0].ensure(sizeof(uint32_t) * total);
-  uint32_t *vals = (uint32_t *)ln.ws[1].ensure(sizeof(uint32_t) * total);
-  J.keys2 = (uint32_t *)ln.ws[2].ensure(sizeof(uint32_t) * total);
-  J.vals2 = (uint32_t *)ln.ws[3].ensure(sizeof(uint32_t) * total);
-  uint32_t *bounds = (uint32_t *)ln.ws[4].ensure(sizeof(uint32_t) * (2 * P.nb + 1));
-  J.bstart = bounds;
-  J.bend = bounds + P.nb;
-  J.valid = bounds + 2 * P.nb;
-  J.ks = 0;
-  {
-    TNS_PROF_ON(ctx, st, "msm_digits", 32.0 * n + 8.0 * total);
-    // the sort's own input (a canonical or u64 SortInput must not be read as Montgomery forms)
-    SortInput din = in;
-    if (!din.fr && !din.u64) {
-      din.fr = scalars;
-      din.mont = true;
-    }
-    k_digits<<<grid_for(n, 256), 256, 0, st>>>(din, n, P.c, P.W, P.sentinel, P.shared, (uint32_t)P.stride,
-                                               keys, vals);
-    TNS_LAUNCH_CHECK();
-  }
-  size_t temp_bytes = 0;
-  TNS_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, J.keys2, vals, J.vals2, (int)total, 0,
-                                             P.end_bit, st));
-  void *temp = ln.ws[9].ensure(temp_bytes);
-  {
-    TNS_PROF_ON(ctx, st, "msm_sort", 16.0 * total);
-    TNS_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, J.keys2, vals, J.vals2, (int)total, 0,
-                                               P.end_bit, st));
-  }
-  TNS_HIP(hipMemsetAsync(bounds, 0, sizeof(uint32_t) * (2 * P.nb + 1), st));
-  k_bucket_bounds<<<grid_for(total, 256), 256, 0, st>>>(J.keys2, total, P.sentinel, J.bstart, J.bend, J.valid);
-  TNS_LAUNCH_CHECK();
-  J.sorted = true;
-  record_now();
+  J.sort_prof.reset(new ProfScope(ctx->prof, st, "msm_sort", 32.0 * n + 16.0 * total));
+  J.valid = (uint32_t *)ln.ws[4].ensure(2 * sizeof(uint32_t));  // entries; [1]: a run crosses a chunk
+  bucket_sort_begin(ln, in, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
+  J.sort_pending = true;
+  J.passes_pending = true;
+  if (!defer) msm_finish_sort(J);
 }
 
 // the bucket sort's passes after pass 1, up to the last pass's readback (no host wait)
@@ -1016,170 +893,153 @@ static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
   }
   MsmLane &ln = *J.lane;
   hipStream_t st = ln.stream;
-  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * J.P.nb);
+  if (!J.buckets) J.buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * J.P.nb);
   HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * J.nchunks);
   {
     TNS_PROF_ON(ctx, st, "msm_accumulate", 96.0 * J.n);  // 96 B per (scalar, point) pair
-    const unsigned acc_cap = ctx->acc_waves > 0 ? (unsigned)(ctx->num_cu * ctx->acc_waves) : (1u << 30);
     uint2 *cbk = (uint2 *)ln.ws[16].ensure(sizeof(uint2) * J.nchunks);
     auto acc = J.keys2 ? k_accumulate<true> : k_accumulate<false>;
-    acc<<<grid_for(J.nchunks, 256, acc_cap), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, buckets, ht, J.nchunks,
-                                                            J.ks, J.acc_k, J.bstart, J.P.nb, cbk);
+    acc<<<grid_for(J.nchunks, 256, 1u << 30), 256, 0, st>>>(J.keys2, J.vals2, J.valid, J.points, J.buckets, ht,
+                                                            J.nchunks, J.ks, J.acc_k, J.bstart, J.P.nb, cbk,
+                                                            J.valid + 1);
     TNS_LAUNCH_CHECK();
   }
   if (accumulated) TNS_HIP(hipEventRecord(accumulated, st));
 }
 
-// the accumulation's tail: bucket fixup, reduction and the per-set sums' readback
-static void msm_launch_tail(Ctx *ctx, MsmJob &J) {
-  if (!J.sorted) return;
-  MsmLane &ln = *J.lane;
-  hipStream_t st = ln.stream;
-  const MsmPlan &P = J.P;
-  uint32_t *keys2 = J.keys2, *bstart = J.bstart, *bend = J.bend, *valid = J.valid;
-  const int ks = J.ks, acc_k = J.acc_k;
-  const size_t nchunks = J.nchunks;
-  G1Xyzz *buckets = (G1Xyzz *)ln.ws[5].p;
-  HeadTail *ht = (HeadTail *)ln.ws[6].p;
+// two sorted MSMs whose tails can run as one two-set launch sequence: the same bucket-set shape
+static bool same_tail_shape(const MsmJob &a, const MsmJob &b) {
+  return a.sorted && b.sorted && a.P.shared == b.P.shared && a.P.Wr == b.P.Wr && a.P.half == b.P.half;
+}
+
+// The accumulation's tail -- bucket fixup, reduction and the per-set sums' readback -- for nj = 1
+// MSM, or nj = 2 of the same shape (same_tail_shape, buckets adjoining: J[1]->buckets ==
+// J[0]->buckets + nb) as ONE sequence of launches on lane `run` whose grids cover both (a pair's two
+// tails side by side on two lanes were short chains at low occupancy each, and the second lane's
+// fixup took 0.97 ms against 0.38 ms for the same work on the first).
+static void msm_launch_tails(Ctx *ctx, MsmJob *const *J, int nj, MsmLane &run) {
+  for (int j = 0; j < nj; j++) {
+    J[j]->res_lane = &run;
+    J[j]->res_set = j;
+    J[j]->res_sets = nj;
+  }
+  if (!J[0]->sorted) return;
+  hipStream_t st = run.stream;
+  const MsmPlan &P = J[0]->P;
+  if (nj == 2 && (!same_tail_shape(*J[0], *J[1]) || J[1]->buckets != J[0]->buckets + P.nb))
+    throw Error(TNS_ERR_DEVICE, "two-set MSM tail over MSMs of different shapes");
   {
     TNS_PROF_ON(ctx, st, "msm_fixup", 0.0);
-    FixLevels F{};
-    size_t groups = nchunks / FIX_FAN, off = 0;
-    while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/F, /F^2, ...
-      F.len[F.n + 1] = groups;
-      off += groups;
-      groups /= FIX_FAN;
-      F.n++;
-    }
-    if (F.n) {
-      G1Xyzz *base = (G1Xyzz *)ln.fix.ensure(sizeof(G1Xyzz) * off);
-      size_t o = 0;
-      for (int l = 1; l <= F.n; l++) {
-        F.lv[l] = base + o;
-        o += F.len[l];
-        k_fix_level<<<grid_for(F.len[l] * FIX_FAN, 256, 1u << 30), 256, 0, st>>>(keys2, valid, ht, F.lv[l - 1], l,
-                                                                                  F.len[l], F.lv[l], ks, acc_k,
-                                                                                  (const uint2 *)ln.ws[16].p);
-        TNS_LAUNCH_CHECK();
+    FixupArgs FA{};
+    int max_levels = 0;
+    size_t max_nb = 0;
+    for (int j = 0; j < nj; j++) {
+      MsmJob &X = *J[j];
+      FixLevels &F = FA.s[j].F;
+      size_t groups = X.nchunks / FIX_FAN, off = 0;
+      while (F.n < FIX_LEVELS && groups >= 2) {  // level sizes: nchunks/F, /F^2, ...
+        F.len[F.n + 1] = groups;
+        off += groups;
+        groups /= FIX_FAN;
+        F.n++;
       }
+      if (F.n) {
+        G1Xyzz *base = (G1Xyzz *)X.lane->fix.ensure(sizeof(G1Xyzz) * off);
+        size_t o = 0;
+        for (int l = 1; l <= F.n; o += F.len[l], l++) F.lv[l] = base + o;
+      }
+      max_levels = std::max(max_levels, F.n);
+      FA.s[j] = FixupSet{X.bstart, X.bend, X.valid, (const HeadTail *)X.lane->ws[6].p, F, X.buckets, X.P.nb, X.acc_k};
+      max_nb = std::max(max_nb, X.P.nb);
     }
-    const char *hv = getenv("TNS_FIX_WAVES");  // =0: every run summed by one thread (A/B)
-    k_bucket_fixup<<<grid_for(P.nb, 256), 256, 0, st>>>(bstart, bend, ht, F, buckets, P.nb, acc_k,
-                                                        !(hv && hv[0] == '0'));
+    for (int l = 1; l <= max_levels; l++) {
+      FixLevelArgs LA{};
+      size_t max_groups = 0;
+      for (int j = 0; j < nj; j++) {
+        const FixLevels &F = FA.s[j].F;
+        const MsmJob &X = *J[j];
+        LA.s[j] = FixLevelSet{X.valid, FA.s[j].ht, F.lv[l - 1], F.lv[l], (const uint2 *)X.lane->ws[16].p,
+                              l <= F.n ? F.len[l] : 0, X.acc_k};
+        if (l <= F.n) max_groups = std::max(max_groups, F.len[l]);
+      }
+      k_fix_level<<<dim3(grid_for(max_groups * FIX_FAN, 256, 1u << 30), nj), 256, 0, st>>>(LA, l);
+      TNS_LAUNCH_CHECK();
+    }
+    k_bucket_fixup<<<dim3(grid_for(max_nb, 256), nj), 256, 0, st>>>(FA);
     TNS_LAUNCH_CHECK();
-    if (const char *fs = getenv("TNS_FIX_STATS"); fs && fs[0] == '1') {  // diagnostics: the runs' chunk spans
-      std::vector<uint32_t> bs(P.nb + 1);
-      uint32_t nvalid = 0;
-      TNS_HIP(hipStreamSynchronize(st));
-      TNS_HIP(hipMemcpy(bs.data(), bstart, sizeof(uint32_t) * (P.nb + 1), hipMemcpyDeviceToHost));
-      TNS_HIP(hipMemcpy(&nvalid, valid, sizeof(uint32_t), hipMemcpyDeviceToHost));
-      size_t cls[7] = {0}, maxspan = 0, maxent = 0, heavy_waves = 0, max_heavy_in_wave = 0;
-      for (size_t w = 0; w * 64 < P.nb; w++) {
-        size_t hw = 0;
-        for (size_t bk = w * 64; bk < std::min(P.nb, w * 64 + 64); bk++) {
-          const uint32_t s = bs[bk], e = bs[bk + 1];
-          const size_t tf = s / acc_k, tl = e > s ? (e - 1) / acc_k : tf, sp = tl - tf;
-          maxspan = std::max(maxspan, sp);
-          maxent = std::max<size_t>(maxent, e - s);
-          cls[s == e ? 0 : sp == 0 ? 1 : sp == 1 ? 2 : sp < 8 ? 3 : sp < 64 ? 4 : sp <= FIX_WAVE_SPAN ? 5 : 6]++;
-          hw += sp > FIX_WAVE_SPAN;
-        }
-        heavy_waves += hw > 0;
-        max_heavy_in_wave = std::max(max_heavy_in_wave, hw);
-      }
-      fprintf(stderr,
-              "[fix-stats] nb %zu entries %u acc_k %d chunks %zu levels %d | empty %zu in-chunk %zu span1 %zu "
-              "span2-7 %zu span8-63 %zu span64-%zu %zu heavy %zu | max span %zu max entries %zu heavy waves %zu "
-              "max heavy per wave %zu\n",
-              P.nb, nvalid, acc_k, nchunks, F.n, cls[0], cls[1], cls[2], cls[3], cls[4], FIX_WAVE_SPAN, cls[5],
-              cls[6], maxspan, maxent, heavy_waves, max_heavy_in_wave);
-    }
   }
   // bucket reduction (see the header): running sums over groups of L0 buckets, then
   // the weighted group sum  sum_g g S_g = sum_b 2^b M_b,  M_b = sum_{g: bit b of g} S_g,
-  // as nbits + 2 plain sums (the M_b and sum_g T_g in two halves) -- short dependency chains only
-  // groups of L0 = 16 buckets (TNS_RED_L; 4 and 8 measured no faster at 2^20, 2 slower);
-  // c >= 4: half >= 8, so g >= 2
-  // up to 2^19 buckets per set the chains are the latency: groups of 4 and masked-sum chunks of 8
-  // (C2, 2^20 points: 2.73 -> 2.65 ms); from 2^21 buckets 16 / 16 stay the fastest (2^22, 2^24)
+  // as nbits + 2 plain sums (the M_b and sum_g T_g in two halves) -- short dependency chains only.
+  // Up to 2^19 buckets per set the chains are the latency: groups of 4 and masked-sum chunks of 8
+  // (C2, 2^20 points: 2.73 -> 2.65 ms); from 2^21 buckets groups of 16 stay the fastest (2^22,
+  // 2^24; 8: +0.19 ms, 32: +0.63 ms per C4 step, r05 A/B).  c >= 4: half >= 8, so g >= 2.
+  const int sets = P.Wr * nj;
   const bool small_sets = P.half <= ((size_t)1 << 19);
-  J.L0 = (int)std::min<size_t>(ctx->red_l > 0 ? ctx->red_l : (small_sets ? 4 : RED_L), P.half / 2);
-  const size_t g1 = P.half / J.L0;
-  // second level (k_reduce_level2) when the first leaves many groups: L1 = 4 (TNS_RED_L1; 0 = off)
+  int L0 = (int)std::min<size_t>(small_sets ? 4 : RED_L, P.half / 2);
+  const size_t g1 = P.half / L0;
+  // a second level (k_reduce_level2, groups of L1 = 4) when the first leaves many groups
   int L1 = g1 >= ((size_t)1 << 13) ? 4 : 0;
-  if (const char *e = getenv("TNS_RED_L1")) L1 = std::max(0, atoi(e));
-  if (L1 && ((L1 & (L1 - 1)) || g1 / L1 < 2)) L1 = 0;  // powers of two, >= 2 groups left
+  if (L1 && g1 / L1 < 2) L1 = 0;
   const size_t g = L1 ? g1 / L1 : g1;
-  J.nbits = 0;
-  while (((size_t)1 << J.nbits) < g) J.nbits++;
-  J.specs = J.nbits + 2;
+  int nbits = 0;
+  while (((size_t)1 << nbits) < g) nbits++;
+  const int specs = nbits + 2;
   {
-    TNS_PROF_ON(ctx, st, "msm_reduce", 128.0 * P.nb);
-    G1Xyzz *T = (G1Xyzz *)ln.ws[7].ensure(sizeof(G1Xyzz) * 2 * P.Wr * (g1 + (L1 ? g : 0)));
-    G1Xyzz *S = T + (size_t)P.Wr * g1;
-    k_reduce_level<<<grid_for((size_t)P.Wr * g1, 64, 1u << 30), 64, 0, st>>>(buckets, P.Wr, P.half, J.L0, T, S);
+    TNS_PROF_ON(ctx, st, "msm_reduce", 128.0 * P.nb * nj);
+    G1Xyzz *T = (G1Xyzz *)run.ws[7].ensure(sizeof(G1Xyzz) * 2 * sets * (g1 + (L1 ? g : 0)));
+    G1Xyzz *S = T + (size_t)sets * g1;
+    k_reduce_level<<<grid_for((size_t)sets * g1, 64, 1u << 30), 64, 0, st>>>(J[0]->buckets, sets, P.half, L0, T, S);
     TNS_LAUNCH_CHECK();
     if (L1) {
-      G1Xyzz *V = S + (size_t)P.Wr * g1, *S2 = V + (size_t)P.Wr * g;
+      G1Xyzz *V = S + (size_t)sets * g1, *S2 = V + (size_t)sets * g;
       int lg0 = 0;
-      while ((1 << lg0) < J.L0) lg0++;
-      k_reduce_level2<<<grid_for((size_t)P.Wr * g, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g1, L1, lg0, V, S2);
+      while ((1 << lg0) < L0) lg0++;
+      k_reduce_level2<<<grid_for((size_t)sets * g, 64, 1u << 30), 64, 0, st>>>(T, S, sets, g1, L1, lg0, V, S2);
       TNS_LAUNCH_CHECK();
       T = V;
       S = S2;
-      J.L0 *= L1;  // the masked sums' weight (msm_complete's doublings)
+      L0 *= L1;  // the masked sums' weight (msm_complete's doublings)
     }
-    const int CH = (int)std::min<size_t>(ctx->red_ch > 0 ? ctx->red_ch : (small_sets || L1 ? 8 : 16), g / 2);
+    const int CH = (int)std::min<size_t>(small_sets || L1 ? 8 : 16, g / 2);
     const size_t nch = g / (2 * (size_t)CH);
-    const size_t nparts = (size_t)P.Wr * J.specs * nch;
-    G1Xyzz *parts = (G1Xyzz *)ln.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)P.Wr * J.specs));
+    const size_t nparts = (size_t)sets * specs * nch;
+    G1Xyzz *parts = (G1Xyzz *)run.ws[8].ensure(sizeof(G1Xyzz) * (2 * nparts + (size_t)sets * specs));
     G1Xyzz *tmp = parts + nparts, *out = tmp + nparts;
-    const char *wt = getenv("TNS_MASKED_TREE");  // =0: per-chunk parts + k_sum_chunks passes (A/B)
-    const bool tree = nch % 64 == 0 && !(wt && wt[0] == '0');
-    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, P.Wr, g, J.nbits, CH, parts, tree);
+    const bool tree = nch % 64 == 0;  // each wave adds its 64 chunk sums by a butterfly
+    k_masked_sums<<<grid_for(nparts, 64, 1u << 30), 64, 0, st>>>(T, S, sets, g, nbits, CH, parts, tree);
     TNS_LAUNCH_CHECK();
-    sum_sets(st, parts, P.Wr * J.specs, tree ? nch / 64 : nch, tmp, out);
-    const size_t fin_n = (size_t)P.Wr * J.specs;
-    // (with the number of sorted non-zero digits = mixed additions of k_accumulate, profiling)
-    if (lane_sync_readback()) {
-      char *h = (char *)ln.host.ensure(sizeof(G1Xyzz) * fin_n + 16);
-      TNS_HIP(hipMemcpyAsync(h, out, sizeof(G1Xyzz) * fin_n, hipMemcpyDeviceToHost, st));
-      TNS_HIP(hipMemcpyAsync(h + sizeof(G1Xyzz) * fin_n, valid, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    } else {
-      const void *src[2] = {out, valid};
-      const size_t by[2] = {sizeof(G1Xyzz) * fin_n, sizeof(uint32_t)};
-      lane_publish(ln, LANE_SLOT_SUMS, 2, src, by);
-    }
+    sum_sets(st, parts, sets * specs, tree ? nch / 64 : nch, tmp, out);
+    // the per-set sums, then each MSM's number of sorted non-zero digits (= mixed additions of
+    // k_accumulate, profiling)
+    const void *src[3] = {out, J[0]->valid, nj == 2 ? J[1]->valid : nullptr};
+    const size_t by[3] = {sizeof(G1Xyzz) * sets * specs, sizeof(uint32_t), sizeof(uint32_t)};
+    lane_publish(run, LANE_SLOT_SUMS, 1 + nj, src, by);
+  }
+  for (int j = 0; j < nj; j++) {
+    J[j]->L0 = L0;
+    J[j]->nbits = nbits;
+    J[j]->specs = specs;
   }
 }
 
 static void msm_launch_reduce(Ctx *ctx, MsmJob &J, hipEvent_t accumulated = nullptr) {
   msm_launch_accumulate(ctx, J, accumulated);
-  msm_launch_tail(ctx, J);
+  MsmJob *one[1] = {&J};
+  msm_launch_tails(ctx, one, 1, *J.lane);
 }
 
-
-static void msm_launch(Ctx *ctx, MsmLane &ln, const G1Affine *points, const Fr *scalars, const SortInput &in,
-                       size_t n, const FixedBase *fb, unsigned bits, MsmJob &J) {
-  msm_launch_sort(ctx, ln, points, scalars, in, n, fb, bits, J);
-  msm_launch_reduce(ctx, J);
-}
-
-// Wait for the lane and finish on the host: R = sum_g T_g + L0 * sum_b 2^b M_b per set,
-// then Horner over the windows (per-window layout).
+// Wait for the tail's readback and finish on the host: R = sum_g T_g + L0 * sum_b 2^b M_b per
+// set, then Horner over the windows (per-window layout).
 static G1Xyzz msm_complete(Ctx *ctx, MsmJob &J) {
   if (J.immediate) return J.result;
-  const void *hp;
-  if (lane_sync_readback()) {
-    TNS_HIP(hipStreamSynchronize(J.lane->stream));
-    hp = J.lane->host.p;
-  } else {
-    hp = lane_wait(*J.lane, LANE_SLOT_SUMS);
-  }
+  const void *hp = lane_wait(J.res_lane ? *J.res_lane : *J.lane, LANE_SLOT_SUMS);
   if (J.tiny) return *(const G1Xyzz *)hp;
   const MsmPlan &P = J.P;
-  const G1Xyzz *fin = (const G1Xyzz *)hp;
-  ctx->prof.add_ops("msm_accumulate", (double)*(const uint32_t *)(fin + (size_t)P.Wr * J.specs));
+  const G1Xyzz *all = (const G1Xyzz *)hp;
+  const G1Xyzz *fin = all + (size_t)J.res_set * P.Wr * J.specs;
+  const uint32_t *cnt = (const uint32_t *)(all + (size_t)J.res_sets * P.Wr * J.specs);
+  ctx->prof.add_ops("msm_accumulate", (double)cnt[J.res_set]);
   std::vector<G1Xyzz> Rw(P.Wr);
   for (int r = 0; r < P.Wr; r++) {
     const G1Xyzz *f = &fin[(size_t)r * J.specs];
@@ -1235,14 +1095,9 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
     if (x.prep) x.prep(ln.stream);
     if (x.n <= 64) return SortInput();
     if (!x.canon_bits) return bits_launch(ln, x.scalars, x.n);
-    if (lane_sync_readback()) {
-      TNS_HIP(hipMemcpyAsync(ln.host.ensure(sizeof(unsigned)), x.canon_bits, sizeof(unsigned), hipMemcpyDeviceToHost,
-                             ln.stream));
-    } else {
-      const void *src[1] = {x.canon_bits};
-      const size_t by[1] = {sizeof(unsigned)};
-      lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
-    }
+    const void *src[1] = {x.canon_bits};
+    const size_t by[1] = {sizeof(unsigned)};
+    lane_publish(ln, LANE_SLOT_BITS, 1, src, by);
     SortInput in;
     if (x.u64) {
       in.u64 = x.u64;
@@ -1294,95 +1149,61 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   cb = start(l1, b);
   if (a.n > 64) ba = bits_result(l0);
   if (b.n > 64) bb = bits_result(l1);
-  hipEvent_t sorted = nullptr, sa = nullptr, sb = nullptr;
-  if (ctx->msm_stagger) TNS_HIP(hipEventCreateWithFlags(&sorted, hipEventDisableTiming));
+  hipEvent_t sa = nullptr, sb = nullptr;
   TNS_HIP(hipEventCreateWithFlags(&sa, hipEventDisableTiming));
   TNS_HIP(hipEventCreateWithFlags(&sb, hipEventDisableTiming));
-  hipEvent_t acc_a_early = nullptr;  // lane 0's accumulation, queued before lane 1's sort
-  if (sorted) {  // staggered: lane 1 sorts under lane 0's accumulation
-    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sorted);
-    TNS_HIP(hipEventRecord(sa, l0.stream));
-    // the accumulation goes in before lane 1's sort reaches its host wait (the last pass's
-    // readback): queued after it, lane 1's first passes would run alone
-    if (ja.sorted) {
-      TNS_HIP(hipEventCreateWithFlags(&acc_a_early, hipEventDisableTiming));
-      msm_launch_accumulate(ctx, ja, acc_a_early);
-    }
-    TNS_HIP(hipStreamWaitEvent(l1.stream, sorted, 0));
-    (void)hipEventDestroy(sorted);
-    // lane 1's sort runs beside that accumulation: the small-register sort kernels, which fit in
-    // what its three waves per SIMD leave free (TNS_SORT_CORUN=0: the full-size kernels, A/B)
-    const char *cr = getenv("TNS_SORT_CORUN");
-    jb.bs.corun = !(cr && cr[0] == '0') && ja.sorted;
-    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb);
-  } else {
-    // both lanes' passes are queued before either lane's host wait (the last pass's readback),
-    // and each lane's last pass follows its own readback: the two sorts run side by side and
-    // neither waits for the other's first passes (TNS_SORT_OVERLAP=0: lane 1's sort is queued
-    // only after lane 0's sort completes, for A/B)
-    const char *ov = getenv("TNS_SORT_OVERLAP");
-    const bool overlap = !(ov && ov[0] == '0');
-    // TNS_SORT_INTERLEAVE=1: both lanes' pass 1 queued before either lane's later passes (A/B)
-    const char *il = getenv("TNS_SORT_INTERLEAVE");
-    const bool interleave = il && il[0] == '1';
-    msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa, overlap);
-    if (!overlap) msm_finish_sort(ja);
-    if (!interleave) msm_sort_passes(ja);
-    msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, overlap);
-    msm_sort_passes(ja);
-    msm_sort_passes(jb);
-    msm_finish_sort(ja);
-    msm_finish_sort(jb);
-  }
-  if (!ctx->msm_stagger) {
-    // both (memory-bound) sorts first, then both accumulations: an accumulation launched
-    // while the other lane still sorts takes every slot and stalls that sort behind it
-    TNS_HIP(hipStreamWaitEvent(l0.stream, sb, 0));
-    TNS_HIP(hipStreamWaitEvent(l1.stream, sa, 0));
-  }
+  // both lanes' passes are queued before either lane's host wait (the last pass's readback), and
+  // each lane's last pass follows its own readback: the two sorts run side by side and neither
+  // waits for the other's first passes (profiles/r02_ab_sort_overlap.txt, r05_ab_sort_overlap.txt)
+  msm_launch_sort(ctx, l0, a.points, a.scalars, ca, a.n, a.fb, ba, ja, sa, true);
+  msm_sort_passes(ja);
+  msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, true);
+  msm_sort_passes(jb);
+  msm_finish_sort(ja);
+  msm_finish_sort(jb);
+  // both (memory-bound) sorts first, then both accumulations: an accumulation launched while the
+  // other lane still sorts takes every slot and stalls that sort behind it
+  TNS_HIP(hipStreamWaitEvent(l0.stream, sb, 0));
+  TNS_HIP(hipStreamWaitEvent(l1.stream, sa, 0));
   (void)hipEventDestroy(sa);
   (void)hipEventDestroy(sb);
-  // TNS_TAILS_LAST: 0 never, 1 always (A/B); default: for a pair of table-window MSMs (the
-  // openings: full-width scalars, ~17 ms accumulations whose tails are ~1.2 ms each)
-  const char *tl = getenv("TNS_TAILS_LAST");
-  const bool tails_last = tl ? tl[0] == '1' : (ja.sorted && jb.sorted && ja.P.shared && jb.P.shared);
-  if (ctx->msm_serial && tails_last) {
-    // the accumulations one after the other (each is VALU-bound on the whole chip: run together
-    // they take as long, and each launch's own duration is then its kernel time), and lane 0's
-    // fixup/reduction waits for lane 1's accumulation: under it, that tail's kernels took wave
-    // slots from the second accumulation; after it the two tails (short chains, few waves each)
-    // run side by side.  (The commitments keep lane 0's tail under lane 1's accumulation: the
-    // 22-bit address MSM's 2^22-bucket reduction is longer than the value accumulation.)
-    hipEvent_t acc_a = acc_a_early, acc_b;
-    if (!acc_a) {
-      TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
-      msm_launch_accumulate(ctx, ja, acc_a);
+  // The accumulations run one after the other (each is VALU-bound on the whole chip: run together
+  // they take as long, and each launch's own duration is then its kernel time).  A pair of
+  // table-window MSMs (the openings: full-width scalars, ~17 ms accumulations) then runs both
+  // tails after the second accumulation as ONE two-set launch sequence on lane 0 (tails under the
+  // second accumulation took wave slots from it, profiles/r02_ab_tails_last.txt); the commitments
+  // keep lane 0's tail under lane 1's accumulation (the 22-bit address MSM's 2^22-bucket reduction
+  // is longer than the value accumulation).
+  const bool tails_last = ja.sorted && jb.sorted && ja.P.shared && jb.P.shared;
+  hipEvent_t acc_a;
+  TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+  if (tails_last) {
+    const bool two_set = same_tail_shape(ja, jb);
+    if (two_set) {  // the pair's buckets adjoin: one reduction over two sets
+      ja.buckets = (G1Xyzz *)l0.ws[5].ensure(sizeof(G1Xyzz) * 2 * ja.P.nb);
+      jb.buckets = ja.buckets + ja.P.nb;
     }
+    hipEvent_t acc_b;
     TNS_HIP(hipEventCreateWithFlags(&acc_b, hipEventDisableTiming));
+    msm_launch_accumulate(ctx, ja, acc_a);
     TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
     msm_launch_accumulate(ctx, jb, acc_b);
     TNS_HIP(hipStreamWaitEvent(l0.stream, acc_b, 0));
-    (void)hipEventDestroy(acc_a);
     (void)hipEventDestroy(acc_b);
-    // (submitting lane 1's tail first measured a tie: 48.51 vs 48.42 ms per step, r05_ab_tail_order.txt)
-    msm_launch_tail(ctx, ja);
-    msm_launch_tail(ctx, jb);
-  } else if (acc_a_early) {  // lane 0's accumulation is queued: its tail, then lane 1's MSM
-    msm_launch_tail(ctx, ja);
-    if (ctx->msm_serial) TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a_early, 0));
-    (void)hipEventDestroy(acc_a_early);
-    msm_launch_reduce(ctx, jb);
-  } else if (ctx->msm_serial) {
-    hipEvent_t acc_a;
-    TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
+    if (two_set) {
+      MsmJob *both[2] = {&ja, &jb};
+      msm_launch_tails(ctx, both, 2, l0);
+    } else {
+      MsmJob *one_a[1] = {&ja}, *one_b[1] = {&jb};
+      msm_launch_tails(ctx, one_a, 1, l0);
+      msm_launch_tails(ctx, one_b, 1, l1);
+    }
+  } else {
     msm_launch_reduce(ctx, ja, acc_a);
     TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
-    (void)hipEventDestroy(acc_a);
-    msm_launch_reduce(ctx, jb);
-  } else {
-    msm_launch_reduce(ctx, ja);
     msm_launch_reduce(ctx, jb);
   }
+  (void)hipEventDestroy(acc_a);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
 }

@@ -169,10 +169,10 @@ class Context:
         when it has tau; False: vector_to_polynomial + coefficient KZG.  Same proofs."""
         _check(N.load().tns_ctx_set_commit_basis(self.handle, 1 if lagrange else 0))
 
-    def set_msm_sort(self, rocprim: bool):
-        """False (default): fused digit + counting bucket sort; True: digit array + rocPRIM
-        radix sort (A/B).  Same results."""
-        _check(N.load().tns_ctx_set_msm_sort(self.handle, 1 if rocprim else 0))
+    def set_upload_chunks(self, chunks: int):
+        """Drop-in provers: the value vector crosses PCIe in `chunks` node ranges (1..64,
+        default 4), each committed as it lands.  Same proofs."""
+        _check(N.load().tns_ctx_set_upload_chunks(self.handle, int(chunks)))
 
     def set_msm_tables(self, on: bool):
         """True (default): MSMs over fixed bases use their window tables (one shared bucket
@@ -1238,7 +1238,12 @@ class Comm:
     def __init__(self, handle: C.c_void_p, rank: int, size: int, keep=None, timeout_s: Optional[float] = None):
         self.handle, self.rank, self.size, self._keep = handle, rank, size, keep
         self.last_failure: Optional[str] = None
-        self.timeout_s = float(timeout_s or self.DEFAULT_TIMEOUT_S)
+        # a host-callback transport whose exchange failed (deadline, transport error) is dead: a
+        # later exchange would pair with a peer's late collective, so it is refused (the RCCL
+        # transport aborts its communicator likewise); tear the process group down to recover
+        self.failed = False
+        # None: the default deadline; 0 or less is the caller's error (tns_comm_set_timeout refuses it)
+        self.timeout_s = self.DEFAULT_TIMEOUT_S if timeout_s is None else float(timeout_s)
         _check(N.load().tns_comm_set_timeout(self.handle, self.timeout_s))
 
     def set_timeout(self, seconds: float):
@@ -1266,17 +1271,23 @@ class Comm:
 
         def cb(user, send, nbytes, recv):
             me = holder.get("comm")
+            if me is not None and me.failed:
+                me.last_failure = ("this communicator failed at an earlier exchange (its collective may still be "
+                                   "pending on a peer); tear the process group down and create a new one")
+                return 4
             try:
                 out = fn(C.string_at(send, nbytes), **({"deadline_s": me.timeout_s} if holder.get("kw") else {}))
                 if len(out) != nbytes * size:
                     if me is not None:
                         me.last_failure = f"allgather returned {len(out)} bytes, expected {nbytes * size}"
+                        me.failed = True
                     return 2
                 C.memmove(recv, out, len(out))
                 return 0
             except Exception as e:  # noqa: BLE001 -- reported to the library as a failed exchange
                 if me is not None:
                     me.last_failure = f"{type(e).__name__}: {e}"
+                    me.failed = True
                 return 3 if isinstance(e, TimeoutError) else 1
         import inspect
 
@@ -1357,12 +1368,13 @@ class Comm:
         return {"rank": r.value, "size": n.value, "seen_size": seen.value, "kind": self.KINDS.get(k.value, "?")}
 
     def stats(self) -> dict:
-        """Exchange steps so far and their host-timed latency (tns_comm_stats)."""
-        out = (C.c_double * 4)()
-        _check(N.load().tns_comm_stats(self.handle, out))
+        """Exchange steps so far, their host-timed latency and this rank's bytes (tns_comm_stats_ex)."""
+        out = (C.c_double * 6)()
+        _check(N.load().tns_comm_stats_ex(self.handle, out))
         n = int(out[0])
         return {"exchanges": n, "total_s": out[1], "mean_us": (out[1] / n * 1e6) if n else None,
-                "max_us": out[2] * 1e6 if n else None, "timeout_s": out[3]}
+                "max_us": out[2] * 1e6 if n else None, "timeout_s": out[3], "bytes_total": out[4],
+                "max_bytes": out[5] if n else None}
 
     def allgather(self, data: bytes, ctx: Optional[Context] = None) -> bytes:
         """The communicator's own allgather (every rank's bytes, in rank order)."""

@@ -94,7 +94,7 @@ SIGNATURES = [
     ("tns_srs_prepare_lagrange_from_powers", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("tns_ctx_set_commit_basis", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_ctx_set_msm_tables", C.c_int, [C.c_void_p, C.c_int]),
-    ("tns_ctx_set_msm_sort", C.c_int, [C.c_void_p, C.c_int]),
+    ("tns_ctx_set_upload_chunks", C.c_int, [C.c_void_p, C.c_int]),
     ("tns_kzg_commit", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
     ("tns_kzg_open", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P, U64P, U64P]),
     ("tns_kzg_commit_evals", C.c_int, [C.c_void_p, C.c_void_p, U64P, C.c_size_t, U64P]),
@@ -167,6 +167,7 @@ SIGNATURES = [
     ("tns_comm_allgather", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("tns_comm_set_timeout", C.c_int, [C.c_void_p, C.c_double]),
     ("tns_comm_stats", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    ("tns_comm_stats_ex", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     ("tns_srs_prepare_lagrange_shard", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_int]),
     ("tns_setup_params_shard", C.c_int,
      [C.c_void_p, C.c_uint, C.c_int, C.c_int, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),

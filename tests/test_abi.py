@@ -166,7 +166,10 @@ def test_comm_timeout_and_stats_abi():
     """A one-rank callback communicator: deadline setter validation and the stats record."""
     lib = N.load()
     comm = ts.Comm.from_allgather(0, 1, lambda b: b, timeout_s=2.5)
-    assert comm.stats() == {"exchanges": 0, "total_s": 0.0, "mean_us": None, "max_us": None, "timeout_s": 2.5}
+    assert comm.stats() == {"exchanges": 0, "total_s": 0.0, "mean_us": None, "max_us": None, "timeout_s": 2.5,
+                            "bytes_total": 0.0, "max_bytes": None}
+    with pytest.raises(ts.InvalidParameters):  # a zero deadline is the caller's error, not the default
+        ts.Comm.from_allgather(0, 1, lambda b: b, timeout_s=0)
     assert lib.tns_comm_set_timeout(comm.handle, 0.0) == 1
     assert lib.tns_comm_set_timeout(comm.handle, -1.0) == 1
     comm.set_timeout(7.0)

@@ -96,6 +96,12 @@ def _deadline_body(rank, world):
         assert "peer ranks still before step 2: [1]" in msg, msg
         st = comm.stats()
         assert st["exchanges"] == 2 and st["max_us"] is not None
+        # the timed-out communicator is dead: a further exchange is refused at once (it would pair
+        # with rank 1's late collective)
+        t1 = time.monotonic()
+        with pytest.raises(ts.DeviceError) as e2:
+            comm.allgather(b"again")
+        assert time.monotonic() - t1 < 1.0 and "failed at an earlier exchange" in str(e2.value)
         return msg
     time.sleep(3.0)
     comm.allgather(b"late")  # completes rank 0's abandoned collective

@@ -136,50 +136,34 @@ def test_shout_c3_full_size_trapdoor():
     spot_check_basis(pp, T, w, ell_t, seed=3)
 
 
-def test_twist_msm_sort_variant_same_proof():
-    """The rocPRIM bucket order (tns_ctx_set_msm_sort) reads the opening quotients in the
-    canonical form the barycentric pass writes and the trace addresses as raw u64: the proof is
-    the same as with the fused counting sort."""
+def test_twist_shout_msm_tables_off_same_proof():
+    """MSMs without the window tables (tns_ctx_set_msm_tables(0): per-window buckets, no
+    precomputation, as the reference's commit, /root/reference/src/commitments.rs:173-177) give
+    the same Twist and Shout proofs as the shared-bucket table plans."""
     L = 14
     pp, _ = params(L)
     addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
+    entries = ts.to_mont([i * i for i in range(5000)])
+    idx = (np.arange(3 << 12, dtype=np.uint64) * 7) % 5000
     a = ts.Twist(pp).prove_soa(addr, val, isw)
+    s_tab = ts.Shout(pp).prove_arrays(entries, idx)
     ctx = pp.commitment_params.srs.ctx
-    ctx.set_msm_sort(True)
+    ctx.set_msm_tables(False)
     try:
         b = ts.Twist(pp).prove_soa(addr, val, isw)
-        entries = ts.to_mont([i * i for i in range(5000)])
-        idx = (np.arange(3 << 12, dtype=np.uint64) * 7) % 5000
-        s_cub = ts.Shout(pp).prove_arrays(entries, idx)
+        s_plain = ts.Shout(pp).prove_arrays(entries, idx)
     finally:
-        ctx.set_msm_sort(False)
+        ctx.set_msm_tables(True)
     assert a == b
-    assert s_cub == ts.Shout(pp).prove_arrays(entries, idx)
+    assert s_tab == s_plain
 
 
-@pytest.mark.parametrize("var", ["TNS_BS_PACK", "TNS_BS_VO", "TNS_BS_K16"])
-@pytest.mark.parametrize("L", [14, 18])
-def test_twist_packed_sort_tail_same_proof(L, var, monkeypatch):
-    """The packed sort tail (the last pass reads one word per entry and writes values only; the
-    accumulation finds its runs from the bucket starts) gives the proof of the key + value sort."""
-    pp, _ = params(L)
-    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
-    a = ts.Twist(pp).prove_soa(addr, val, isw)
-    monkeypatch.setenv(var, "0")
-    b = ts.Twist(pp).prove_soa(addr, val, isw)
-    assert a == b
-
-
-@pytest.mark.parametrize("chunks", ["1", "3", "4", "7", "4/split", "3/split"])
-def test_twist_dropin_chunked_value_commitment(chunks, monkeypatch):
+@pytest.mark.parametrize("chunks", [1, 3, 4, 7])
+def test_twist_dropin_chunked_value_commitment(chunks):
     """The drop-in prover commits the value vector chunk by chunk as its upload lands
-    (TNS_UPLOAD_CHUNKS node ranges, the last one split in two with TNS_UPLOAD_SPLIT_LAST=1; one
-    MSM each, summed): full-width values take the window-table plan at each chunk's offset, the
-    bench trace's narrow values the per-window plan; both equal the device-resident proof (one MSM
-    over the whole vector)."""
-    chunks, _, split = chunks.partition("/")
-    if split:
-        monkeypatch.setenv("TNS_UPLOAD_SPLIT_LAST", "1")
+    (tns_ctx_set_upload_chunks node ranges; one MSM each, summed): full-width values take the
+    window-table plan at each chunk's offset, the bench trace's narrow values the per-window plan;
+    both equal the device-resident proof (one MSM over the whole vector)."""
     L = 16
     pp, _ = params(L)
     n = 1 << (L + 2)
@@ -188,29 +172,19 @@ def test_twist_dropin_chunked_value_commitment(chunks, monkeypatch):
     wide = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * 2 + rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
     wide[:, 3] &= np.uint64(0x0FFFFFFFFFFFFFFF)
     ctx = pp.commitment_params.srs.ctx
-    monkeypatch.setenv("TNS_UPLOAD_CHUNKS", chunks)
-    for v in (val, wide):
-        d = [ts.DeviceBuffer(ctx, x) for x in (addr, v, isw)]
-        want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
-        assert ts.Twist(pp).prove_soa(addr, v, isw) == want
+    ctx.set_upload_chunks(chunks)
+    try:
+        for v in (val, wide):
+            d = [ts.DeviceBuffer(ctx, x) for x in (addr, v, isw)]
+            want = ts.twist_proof_from_raw(ts.twist_prove_resident(pp, *d, n))
+            assert ts.Twist(pp).prove_soa(addr, v, isw) == want
+    finally:
+        ctx.set_upload_chunks(4)
 
 
-@pytest.mark.parametrize("corun", ["1", "0"])
-@pytest.mark.parametrize("L", [14, 18])
-def test_twist_staggered_corun_sort_same_proof(L, corun, monkeypatch):
-    """The staggered two-lane MSM schedule (TNS_MSM_STAGGER=1, read at context creation): lane 1's
-    bucket sort runs beside lane 0's accumulation with the small-register kernels (2048-entry
-    tiles, BucketSortJob::corun), or with the full-size ones (TNS_SORT_CORUN=0).  Same proof as
-    the default schedule, Twist and Shout."""
-    pp, _ = params(L)
-    addr, val, isw = ts.bench_trace(1 << L, 1 << (L + 2))
-    want = ts.Twist(pp).prove_soa(addr, val, isw)
-    entries = ts.to_mont([i * i + 3 for i in range(1 << 12)])
-    idx = (np.arange(1 << (L + 1), dtype=np.uint64) * 7) % (1 << 12)
-    want_s = ts.Shout(pp).prove_arrays(entries, idx)
-    monkeypatch.setenv("TNS_MSM_STAGGER", "1")
-    monkeypatch.setenv("TNS_SORT_CORUN", corun)
-    ctx = ts.Context(0)
-    pp2, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
-    assert ts.Twist(pp2).prove_soa(addr, val, isw) == want
-    assert ts.Shout(pp2).prove_arrays(entries, idx) == want_s
+def test_upload_chunks_out_of_range():
+    pp, _ = params(10)
+    ctx = pp.commitment_params.srs.ctx
+    for bad in (0, -1, 65):
+        with pytest.raises(ts.InvalidParameters):
+            ctx.set_upload_chunks(bad)

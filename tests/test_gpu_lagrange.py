@@ -130,10 +130,11 @@ def test_twist_proof_identical_on_both_paths(logn):
     assert a == b
 
 
-def test_chain_inverse_batch_matches_fermat(monkeypatch):
-    """k_chain_inv (one batch inversion per block of 256 chains) == one Fermat inverse per chain
-    (TNS_CHAIN_INV=0) on the opening paths with chains of several nodes: Twist at 2^18 (the
-    two-vector k_node_finish2) and Shout with T != M (two single-vector openings)."""
+def test_chain_inverse_openings_match_coefficient_route():
+    """The openings' batch chain inversion (k_chain_inv: one inversion per block of 256 chains,
+    chains of several nodes from 2^18 on) against the coefficient route (interpolation +
+    coefficient KZG, no inversion at all): Twist at 2^18 (the two-vector k_node_finish2) and Shout
+    with T != M (two single-vector openings) give the same proofs."""
     pp, _ = params(17)  # SRS 2^19 + 1 points
     n = 1 << 18
     pp.commitment_params.srs.prepare_lagrange(n)
@@ -143,8 +144,12 @@ def test_chain_inverse_batch_matches_fermat(monkeypatch):
     entries = ts.to_mont(rand_vals(T, seed=11))
     idx = rng.integers(0, T, size=M, dtype=np.uint64)
     a = (ts.Twist(pp).prove_soa(addr, val, isw), ts.Shout(pp).prove_arrays(entries, idx))
-    monkeypatch.setenv("TNS_CHAIN_INV", "0")
-    b = (ts.Twist(pp).prove_soa(addr, val, isw), ts.Shout(pp).prove_arrays(entries, idx))
+    ctx = pp.commitment_params.srs.ctx
+    ctx.set_commit_basis(False)
+    try:
+        b = (ts.Twist(pp).prove_soa(addr, val, isw), ts.Shout(pp).prove_arrays(entries, idx))
+    finally:
+        ctx.set_commit_basis(True)
     assert a == b
 
 

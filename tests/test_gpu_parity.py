@@ -162,50 +162,63 @@ def test_msm_window_tables_equal_per_window_layout(logn):
         assert a == b
 
 
-@pytest.mark.parametrize("variant", ["TNS_BS_RUNTIME_PASS1", "TNS_BS_NO_LOCAL_LAST", "TNS_MSM_W1", "TNS_FIX_WAVES",
-                                     "TNS_BS_TILES", "TNS_MASKED_TREE", "TNS_ACC_ROUNDS", "TNS_BS_PACK", "TNS_BS_VO", "TNS_BS_K16",
-                                     "TNS_BS_K16=2", "TNS_RED_L1=0", "TNS_RED_L1=8", "TNS_BS_BITS=last+1",
-                                     "TNS_BS_GEOM=0", "TNS_MSM_SYNC_READBACK=1"])
+def trapdoor_commitment(tau, vals):
+    """(sum_i c_i tau^i) G -- the commitment by the SRS's retained tau (oracle side)."""
+    s = 0
+    for v in reversed(vals):
+        s = (s * tau + v) % R
+    return po.affine_mul(po.G1_GEN, s)
+
+
+@pytest.mark.parametrize("tables", [True, False])
 @pytest.mark.parametrize("pattern", ["full", "addr21", "addr22", "val30", "equal"])
-def test_msm_bucket_sort_variants_agree(pattern, variant, monkeypatch):
-    """The bucket sort's fast paths == its general kernels: the compile-time-plan pass 1 (c = 20,
-    W = 13 table windows at 2^20; the per-window c = 12 / 16, W = 2 plans of narrow scalars) vs
-    the runtime-plan kernels, the all-one-tile last pass vs the tiled one, the single
-    22-bit window of 21-bit scalars vs two windows (TNS_MSM_W1=0), and runs over many chunks
-    summed by one wave each vs one thread each (TNS_FIX_WAVES=0; "equal": one run per window
-    spans every chunk), half-size pass-1 tiles (TNS_BS_TILES=4096,...: the compile-time plan's
-    4096-entry variant for the table windows), the masked sums' per-chunk parts vs their
-    wave butterfly (TNS_MASKED_TREE=0) and the accumulation's round-filling chunk size (70 entries
-    per thread for the full-width case, every pattern with TNS_ACC_ROUNDS=1) vs the power-of-two
-    rule (32), and the packed sort tail (one word per entry into the last pass, values only out
-    of it, runs found from the bucket starts) vs keys and values throughout (TNS_BS_PACK=0; the
-    table stride here is 2^20 + 1, so the packed index is recovered by a multiply), and the
-    values-only last pass vs keys + values out of it (TNS_BS_VO=0: the accumulation reads keys),
-    and 16-bit keys into the last pass vs 32-bit ones (TNS_BS_K16=0) or 16-bit keys out of every
-    pass, the 17th key bit of pass 1's output carried in bit 30 of the value (TNS_BS_K16=2), and
-    the bucket reduction's second level (k_reduce_level2, L1 = 4 by default) off (TNS_RED_L1=0:
-    masked sums straight over the first level's groups) or with groups of 8, and one key bit moved
-    from the first sort pass to the last (TNS_BS_BITS=last+1: a 9-bit last pass becomes the
-    1024-bin kernels), and the sort geometry as tile counts + scans instead of one launch
-    (TNS_BS_GEOM=0) and the MSM's host readbacks as pinned copies + a stream synchronize instead of
-    the published flag (TNS_MSM_SYNC_READBACK=1)."""
+def test_msm_sort_shapes_trapdoor(pattern, tables):
+    """The bucket sort's plans at 2^20 pairs, each against the trapdoor identity (not against
+    another HIP path): full-width scalars (the c = 20, W = 13 table plan, or 13 per-window
+    buckets sets without the table: the runtime-plan pass-1 kernels), 21- and 22-bit scalars (the
+    single 22/23-bit window: 2^21/2^22 buckets, the per-window packed tail), 30-bit values (W = 2,
+    c = 16: the per-window compile-time plan and its heavy buckets across many chunks), and one
+    value repeated (every entry of a window in one bucket: the fixup's wave-summed runs)."""
     pp, _ = params(18)
     n = 1 << 20
     rng = np.random.default_rng(len(pattern))
     if pattern == "full":
         c = rand_fr_mont(n, seed=77)
+        vals = ts.from_mont(c)
     elif pattern == "equal":
-        c = ts.to_mont([R - 12345] * n)
+        vals = [R - 12345] * n
+        c = ts.to_mont(vals)
     else:
         bits = int(pattern[-2:])
-        c = ts.fr_from_u64_array(rng.integers(0, 1 << bits, size=n, dtype=np.uint64))
-    a = ts.msm(pp.commitment_params, c)
-    value = {"TNS_MSM_W1": "0", "TNS_FIX_WAVES": "0", "TNS_BS_PACK": "0", "TNS_BS_VO": "0", "TNS_BS_K16": "0", "TNS_MASKED_TREE": "0", "TNS_BS_TILES": "4096,8192,4096",
-             "TNS_ACC_ROUNDS": "0" if pattern == "full" else "1"}
-    name, _, forced = variant.partition("=")
-    monkeypatch.setenv(name, forced or value.get(variant, "1"))
-    b = ts.msm(pp.commitment_params, c)
-    assert a == b
+        u = rng.integers(0, 1 << bits, size=n, dtype=np.uint64)
+        vals = [int(x) for x in u]
+        c = ts.fr_from_u64_array(u)
+    ctx = pp.commitment_params.srs.ctx
+    ctx.set_msm_tables(tables)
+    try:
+        got = ts.msm(pp.commitment_params, c)
+    finally:
+        ctx.set_msm_tables(True)
+    assert got == trapdoor_commitment(pp.commitment_params.tau, vals)
+
+
+@pytest.mark.parametrize("tables", [True, False])
+def test_msm_c2_bench_workload_trapdoor(tables):
+    """The exact C2 bench input -- Fr::rand from ChaCha20Rng([7; 32]), 2^20 scalars
+    (ts.fr_rand_batch, the reference's UniformRand restated) over setup_params(18), device-resident
+    as bench.py passes them -- against C == (sum c_i tau^i) G, with the SRS window table and
+    without it (/root/reference/src/commitments.rs:162-180)."""
+    pp, _ = params(18)
+    n = 1 << 20
+    sc = ts.fr_rand_batch(bytes([7] * 32), n)
+    ctx = pp.commitment_params.srs.ctx
+    d = ts.DeviceBuffer(ctx, sc)
+    ctx.set_msm_tables(tables)
+    try:
+        got = ts.msm_resident(pp.commitment_params, d, n)
+    finally:
+        ctx.set_msm_tables(True)
+    assert ts._g1_from_proj(got) == trapdoor_commitment(pp.commitment_params.tau, ts.from_mont(sc))
 
 
 def test_commit_beyond_srs_is_commitment_error():
@@ -366,7 +379,7 @@ COMPOSITIONS = {
 
 
 @pytest.mark.parametrize("name", list(COMPOSITIONS))
-@pytest.mark.parametrize("nv", [1, 3, 6])
+@pytest.mark.parametrize("nv", [0, 1, 3, 6])
 def test_sumcheck_matches_oracle(name, nv):
     terms = COMPOSITIONS[name]
     tabs = [rand_fr_mont(1 << nv, seed=nv * 31 + i) for i in range(3)]

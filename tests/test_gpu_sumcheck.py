@@ -89,27 +89,24 @@ def test_generic_sumcheck_wrong_claim_at_scale():
 
 
 @pytest.mark.parametrize("name", ["twist_like", "dense4"])
-@pytest.mark.parametrize("env", ["TNS_SC_PREQUEUE=0", "TNS_SC_TAIL_LOG=0", "TNS_SC_TAIL_LOG=11", "TNS_SC_TAIL_BLOCKS=1",
-                                 "TNS_SC_TAIL_BLOCKS=1024", "TNS_SC_SPLIT_LOG=0", "TNS_SC_SPLIT_LOG=16", "TNS_SC_FOLD3=0"])
-def test_generic_sumcheck_schedules_agree(name, env, monkeypatch):
-    """The round schedule's alternatives give the same proof as the oracle: rounds queued after
-    their challenge instead of behind a device wait (PREQUEUE=0), no persistent tail kernel
-    (TAIL_LOG=0) or one taking over only from 2^11 pairs (round 4, not 2), the tail on one block (its rounds' pairs in
-    one wave, the grid barrier trivial) or on 1024, the four-lanes-a-pair split kernel never
-    (SPLIT_LOG=0) or up to 2^16 pairs, and one launch a round instead of the fused folds."""
-    nv = 16
+@pytest.mark.parametrize("nv", [0, 1, 2, 3, 4, 5, 13, 14, 15, 16])
+def test_generic_sumcheck_schedule_regimes(name, nv):
+    """Every regime of the round schedule against the fold oracle: nv = 0 (the final kernel reads
+    the caller's tables as they are), nv = 1 (round 0 then the final fold of the caller's
+    tables), 2..5 (the persistent tail from round 2 on), 13..16 (split four-lanes-a-pair rounds up
+    to 2^13 pairs, the pairs-per-lane kernel above, the tail taking over at 2^13 pairs) -- host
+    and device-resident entry points alike."""
     terms = COMPOSITIONS[name]
     k = 1 + max(max(ix) for _, ix in terms if ix)
-    tabs = rand_tables(k, nv, seed=41 + k)
+    tabs = rand_tables(k, nv, seed=41 + k + nv)
     T = host_threads()
     claim = co.fast_composition_sum(tabs, nv, terms, T)
     st, rounds, fin, chal = co.fast_sumcheck_prove(tabs, nv, claim, terms, threads=T)
     assert st == 0
-    var, _, val = env.partition("=")
-    monkeypatch.setenv(var, val)
     ctx = ts.Context.get(0)
     d = [ts.DeviceBuffer(ctx, t) for t in tabs]
-    proof, chals = ts.SumCheck(nv, claim).prove_resident(d, terms, ts.Transcript(bytes(32)))
-    assert proof.round_polynomials == [co.fr_ints(r) for r in rounds]
-    assert proof.final_evaluation == co.fr_ints(fin)[0]
-    assert chals == co.fr_ints(chal)
+    for proof, chals in (ts.SumCheck(nv, claim).prove(tabs, terms, ts.Transcript(bytes(32)), return_challenges=True),
+                         ts.SumCheck(nv, claim).prove_resident(d, terms, ts.Transcript(bytes(32)))):
+        assert proof.round_polynomials == [co.fr_ints(r) for r in rounds]
+        assert proof.final_evaluation == co.fr_ints(fin)[0]
+        assert chals == co.fr_ints(chal)
