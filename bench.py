@@ -103,6 +103,12 @@ def parse():
                     help="testing aid: every rank on device 0 with a gloo process group (one-GPU box)")
     ap.add_argument("--no-msm-tables", action="store_true",
                     help="per-window MSM buckets instead of the fixed-base window tables")
+    ap.add_argument("--no-table-steps", type=int, default=3,
+                    help="N = 1 extra: C4 proofs timed with the MSM window tables off (per-window buckets, no "
+                         "precomputation beyond the Lagrange basis), proof checked equal (0: skip)")
+    ap.add_argument("--c5-steps", type=int, default=2,
+                    help="N = 1 extra: C5 (one 2^26-op proof, setup_params(24)) on this one GPU, timed over "
+                         "this many steps -- the same-work denominator of the N > 1 strong-scaling lines (0: skip)")
     ap.add_argument("--stage-steps", type=int, default=2,
                     help="untimed steps after the timed region that time every stage (stages_ms_per_step); "
                          "the timed steps time only the roofline kernel (two HIP events per launch)")
@@ -560,15 +566,38 @@ def per_rank_exchange_record(pg, rank, dt, steps, s0, s1):
     steps (tns_comm_stats deltas), gathered to every rank in rank order."""
     n = s1["exchanges"] - s0["exchanges"]
     tot = s1["total_s"] - s0["total_s"]
+    by = s1["bytes_total"] - s0["bytes_total"]
     mine = {"rank": rank, "ms_per_step": round(dt / max(1, steps) * 1e3, 3),
             "exchanges_per_step": round(n / max(1, steps), 2),
             "mean_exchange_us": round(tot / n * 1e6, 1) if n else None,
-            "max_exchange_us_so_far": round(s1["max_us"], 1) if s1["max_us"] is not None else None}
+            "max_exchange_us_so_far": round(s1["max_us"], 1) if s1["max_us"] is not None else None,
+            "mean_exchange_bytes_per_rank": round(by / n, 1) if n else None,
+            "max_exchange_bytes_per_rank": s1["max_bytes"]}
     if pg is None:
         return [mine]
     allv = [None] * pg.get_world_size()
     pg.all_gather_object(allv, mine)
     return allv
+
+
+def c5_one_gpu(ts, ctx, local, steps):
+    """C5's work on this one GPU: ONE Twist::prove of the 2^26-op trace over setup_params(24), trace
+    resident -- the same-work N = 1 point of the strong-scaling curve the N > 1 lines (C5 sharded)
+    are divided by.  Setup (SRS, Lagrange basis, window table) outside the timing, as for C4."""
+    t0 = time.perf_counter()
+    pp5, _ = ts.setup_params(24, device=local)
+    pp5.commitment_params.srs.prepare_lagrange(1 << 26)
+    n5 = 1 << 26
+    addr, val, isw = ts.bench_trace(1 << 24, n5)
+    d = [ts.DeviceBuffer(ctx, x) for x in (addr, val, isw)]
+    del addr, val, isw
+    setup_s = time.perf_counter() - t0
+    t = timed_proofs(lambda: ts.twist_prove_resident(pp5, *d, n5), steps, 1)
+    rec = {"workload": "C5 on one GPU: Twist::prove, 2^26-op trace, setup_params(24), trace resident",
+           "steps": steps, "ms_per_step": round(t * 1e3, 3), "ops_per_sec": round(n5 / t, 2),
+           "setup_s": round(setup_s, 2)}
+    del d, pp5
+    return rec
 
 
 def timed_proofs(fn, steps, warmup):
@@ -768,6 +797,21 @@ def main():
         out["msm_2^20_no_table_same_commitment"] = same
         out["msm_2^20_table_note"] = ("msm_*_2^20: fixed-base window table over the SRS (built once at setup, "
                                       "T[j n + i] = 2^(c j) g1_powers[i]); *_no_table: variable-base, no precomputation")
+        # C4 with no window tables: the reference's commit has no precomputation
+        # (src/commitments.rs:173-177); every MSM of the step runs per-window buckets over the
+        # Lagrange basis itself, and the proof must be the one the table plans gave
+        if args.no_table_steps > 0 and not args.no_msm_tables:
+            want = bytes(prove())
+            ctx.set_msm_tables(False)
+            try:
+                t_nt = timed_proofs(prove, args.no_table_steps, 1)
+                same_nt = bytes(prove()) == want
+            finally:
+                ctx.set_msm_tables(True)
+            out["ms_per_step_no_table"] = round(t_nt * 1e3, 3)
+            out["twist_ops_per_sec_no_table"] = round(n_ops / t_nt, 2)
+            out["no_table_steps"] = args.no_table_steps
+            out["no_table_same_proof"] = same_nt
         # C3: Shout, 2^20 squares table, 2^20 lookups i % 2^20 (src/benchmarks.rs:167-177)
         T = 1 << 20
         entries = ts.fr_from_u64_array(np.arange(T, dtype=np.uint64) ** 2)
@@ -776,6 +820,9 @@ def main():
         t_sh = timed_proofs(lambda: ts.shout_prove_resident(pp18, d_e, T, d_i, T), 5, 1)
         out["shout_lookups_per_sec_2^20"] = round(T / t_sh, 1)
         out["shout_ms_2^20"] = round(t_sh * 1e3, 3)
+    if rank == 0 and world == 1 and not args.no_extras and args.c5_steps > 0 and log_total == 24:
+        out["c5_one_gpu"] = c5_one_gpu(ts, ctx, local, args.c5_steps)
+        out["c5_one_gpu_ms_per_step"] = out["c5_one_gpu"].get("ms_per_step")
     if sharded and not args.no_extras:  # the MSM half of the metric at N GPUs (C2 sharded)
         with exchange_guard(ts, rank, "KZG MSM 2^20 (sharded)"):
             out.update(sharded_msm(ts, ctx, comm, pg, local, rank, world))

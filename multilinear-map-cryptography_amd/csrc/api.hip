@@ -304,15 +304,30 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
     }
   for (int k = 0; k < 2; k++) value[k] = mul(ell[k], S[k]);  // P(z) = ell(z) sum_j w_j y_j / (z - j)
   unsigned *qbits = canon_q ? (unsigned *)c->qbits.ensure(2 * sizeof(unsigned)) : nullptr;
-  if (same_nodes) {
+  // the shared-table plan both opening MSMs will take (full-width quotients): the quotient kernel
+  // also counts pass 1 of both bucket sorts (their count kernels and one read of q0 / q1 go)
+  const FixedBase *f0 = p0.basis->fb, *f1 = p1.basis->fb;
+  const uint32_t *pre[2] = {nullptr, nullptr};
+  bool fused = false;
+  if (same_nodes && canon_inv && c->msm_tables && f0 && f1 && f0->c == f1->c && f0->W == f1->W)
+    fused = quotient2_count_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1, qbits, f0->c, f0->W, pre);
+  if (fused) {
+  } else if (same_nodes) {
     lagrange_quotient_finish2_dev(c, p0.y, p1.y, p0.cnt, value[0], value[1], q1, q0, q1, qbits, canon_inv);
   } else {
     lagrange_quotient_finish_dev(c, p0.y, p0.cnt, value[0], q0);
     lagrange_quotient_finish_dev(c, p1.y, p1.cnt, value[1], q1);
   }
   G1Xyzz pp[2];
-  msm_pair_dev(c, MsmArgs{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits},
-               MsmArgs{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr}, pp);
+  MsmArgs a0{p0.basis->points.as<G1Affine>(), q0, p0.cnt, p0.basis->fb, qbits};
+  MsmArgs a1{p1.basis->points.as<G1Affine>(), q1, p1.cnt, p1.basis->fb, qbits ? qbits + 1 : nullptr};
+  if (fused) {  // (lane 0 sorts a0, lane 1 a1: neither is late)
+    a0.precounted = pre[0];
+    a1.precounted = pre[1];
+    a0.pre_c = a1.pre_c = f0->c;
+    a0.pre_W = a1.pre_W = f0->W;
+  }
+  msm_pair_dev(c, a0, a1, pp);
   if (extra && extra_ready) extra_ready();
   allgather_sum_g1_pair(c, m, pp, proof, extra ? "opening pair partial MSMs + folded table values" : "opening pair partial MSMs",
                         extra);

@@ -811,6 +811,37 @@ static void exclusive_scan(hipStream_t st, DevBuf &tmp, const uint32_t *in, uint
   TNS_LAUNCH_CHECK();
 }
 
+// Pass 1's geometry for W*n entries of `bucket_bits`-bit buckets: key bits and passes, the
+// compile-time plan (if any), scalars per tile, tiles, bins, shift and the count buffer's length
+struct Pass1Geom {
+  int keybits = 0, npass = 0, wb = 0, bits0 = 0, nb = 0, shift = 0;
+  const Pass1Plan *ct = nullptr;
+  size_t spb = 0, T1 = 0, cnt_len = 0;
+};
+static Pass1Geom pass1_geom(size_t n, int c, int W, bool shared, int bucket_bits) {
+  Pass1Geom g;
+  if (shared)
+    while ((1 << g.wb) < W) g.wb++;
+  g.keybits = bucket_bits + g.wb;
+  g.npass = std::max(1, (g.keybits + BS_MAXBITS - 1) / BS_MAXBITS);
+  // the last pass sorts LDS-sized segments by BS_MAXBITS bits; the passes before it split the
+  // remaining bits evenly (25-bit keys: 8, 8, 9 -- pass 2 with 256 instead of 512 bins writes
+  // 128-byte runs: 1.21 -> 1.02 ms at 2^24)
+  const int last = std::min(g.keybits, BS_MAXBITS);
+  g.bits0 = g.npass == 1 ? last : (g.keybits - last + (g.npass - 2)) / (g.npass - 1);
+  g.nb = 1 << g.bits0;
+  g.shift = g.keybits - g.bits0;
+  for (const Pass1Plan &p : kPass1Plans)
+    if (p.tile == BS_TILE && p.c == c && p.W == W) g.ct = &p;
+  g.spb = (size_t)BS_TILE / W;
+  if (g.ct) g.spb = std::min(g.spb, (size_t)BS_BLOCK * g.ct->spt);
+  g.T1 = (n + g.spb - 1) / g.spb;
+  const size_t E = (size_t)W * n, max_seg = (size_t)1 << g.keybits, tmin = 4096;
+  const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> last) + 1;
+  g.cnt_len = std::max((size_t)g.nb * g.T1, (size_t)BS_MAXBINS * max_tiles) + 1;
+  return g;
+}
+
 // Groups the W*n digit entries of `scalars` by bucket (bucket_bits bits of bucket index;
 // per-window layout: window bits included).  The result (BucketOrder): the key/value arrays
 // holding it (two of the lane's four entry buffers), the bucket starts (bucket b =
@@ -888,6 +919,9 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   if (ct) A.spb = std::min(A.spb, (size_t)BS_BLOCK * ct->spt);
   const size_t T1 = (n + A.spb - 1) / A.spb;
   int nb = 1 << bits[0];
+  const Pass1Geom pg = pass1_geom(n, c, W, shared, bucket_bits);
+  if (pg.bits0 != bits[0] || pg.T1 != T1 || pg.ct != ct || pg.shift != shift)
+    throw Error(TNS_ERR_DEVICE, "bucket sort: pass-1 geometry mismatch");
   const size_t max_seg = (size_t)1 << keybits;
   uint32_t **seg = J.seg;
   seg[0] = (uint32_t *)ln.ws[10].ensure(sizeof(uint32_t) * (max_seg + 1));
@@ -895,11 +929,15 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   const size_t tmin = 4096;  // the smallest pass tile
   const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> bits[npass - 1]) + 1;
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
+  const bool pre = in.precounted && shared && ct && in.pre_c == c && in.pre_W == W && ln.ws[12].p == in.precounted &&
+                   ln.ws[12].bytes >= sizeof(uint32_t) * cnt_len;
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
-  if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
-  else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
-  TNS_LAUNCH_CHECK();
+  if (!pre) {  // (precounted: quotient2_count_dev wrote them)
+    if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+    else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+    TNS_LAUNCH_CHECK();
+  }
   exclusive_scan(st, ln.ws[9], counts, offs, (size_t)nb * T1 + 1);
   const int kf1 = npass > 1 ? J.kf[0] : KF_U32;
   if (ct) ct->scatter<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, offs, kf1, K[0], V[0]);
@@ -1043,6 +1081,60 @@ BucketOrder bucket_sort_finish(BucketSortJob &J) {
     TNS_LAUNCH_CHECK();
   }
   return BucketOrder{J.vo ? nullptr : J.K[J.cur], J.V[J.cur], bstart, J.wb, entries};
+}
+
+// The opening quotients (lagrange.hip k_node_quotient2_canon<true>) fused with both sorts' pass-1
+// histograms (k_bs_count1_ct): one block per pass-1 tile of spb nodes; the block writes q0 / q1,
+// their bit lengths, and each quotient's digits' bins into two LDS histograms.
+template <int C, int W>
+__global__ void __launch_bounds__(BS_BLOCK) k_quotient2_count1(const Fr *__restrict__ y0, const Fr *__restrict__ y1,
+                                                               Fr v0, Fr v1, size_t n, const Fr *invs,
+                                                               Fr *__restrict__ q0, Fr *q1, unsigned *__restrict__ bits,
+                                                               size_t spb, int wb, int shift, int nbins, size_t T1,
+                                                               uint32_t *__restrict__ counts0,
+                                                               uint32_t *__restrict__ counts1) {
+  __shared__ uint32_t h0[BS_MAXBINS], h1[BS_MAXBINS];
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h0[d] = h1[d] = 0;
+  __syncthreads();
+  DigitArgs A{};
+  A.shared = true;
+  A.wb = wb;
+  const size_t tile = blockIdx.x, a = tile * spb, b = min(n, a + spb);
+  unsigned b0 = 0, b1 = 0;
+  for (size_t i = a + threadIdx.x; i < b; i += BS_BLOCK) {
+    const Fr iv = invs[i];  // (q1 may be invs itself: each i is read, then written, by one thread)
+    const Fr c0 = mul(sub(v0, y0[i]), iv), c1 = mul(sub(v1, y1[i]), iv);
+    q0[i] = c0;
+    q1[i] = c1;
+    b0 = max(b0, fr_bit_length(c0));
+    b1 = max(b1, fr_bit_length(c1));
+    scalar_digits_ct<C, W>(c0, A, [&](int, uint32_t key, bool) { atomicAdd(&h0[key >> shift], 1u); });
+    scalar_digits_ct<C, W>(c1, A, [&](int, uint32_t key, bool) { atomicAdd(&h1[key >> shift], 1u); });
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) {
+    counts0[(size_t)d * T1 + tile] = h0[d];
+    counts1[(size_t)d * T1 + tile] = h1[d];
+  }
+  if (tile == 0 && threadIdx.x == 0) counts0[(size_t)nbins * T1] = counts1[(size_t)nbins * T1] = 0;
+  block_atomic_max2(b0, b1, bits, bits + 1);
+}
+
+bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr &v0, const Fr &v1, const Fr *inv,
+                         Fr *q0, Fr *q1, unsigned *bits, int cw, int W, const uint32_t *counts_out[2]) {
+  if (cw != 22 || W != 12) return false;  // (the openings' table plan at 2^21..2^26 nodes; else unfused)
+  const Pass1Geom g = pass1_geom(n, cw, W, true, cw - 1);
+  if (!g.ct || g.npass < 2) return false;
+  uint32_t *cnt[2];
+  for (int k = 0; k < 2; k++) cnt[k] = (uint32_t *)c->lanes[k].ws[12].ensure(sizeof(uint32_t) * g.cnt_len);
+  TNS_PROF(c, "open_scan", 32.0 * 5 * n);
+  TNS_HIP(hipMemsetAsync(bits, 0, 2 * sizeof(unsigned), c->stream));
+  k_quotient2_count1<22, 12><<<(unsigned)g.T1, BS_BLOCK, 0, c->stream>>>(y0, y1, v0, v1, n, inv, q0, q1, bits, g.spb, g.wb,
+                                                                          g.shift, g.nb, g.T1, cnt[0], cnt[1]);
+  TNS_LAUNCH_CHECK();
+  counts_out[0] = cnt[0];
+  counts_out[1] = cnt[1];
+  return true;
 }
 
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,

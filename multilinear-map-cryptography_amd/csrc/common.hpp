@@ -494,6 +494,9 @@ struct MsmArgs {
   // else `scalars` themselves (n > 64 only: the tiny path reads Montgomery scalars)
   const unsigned *canon_bits = nullptr;
   const Fr *canon = nullptr;
+  // set (with canon_bits, canonical scalars): pass 1's histograms are precounted (SortInput::precounted)
+  const uint32_t *precounted = nullptr;
+  int pre_c = 0, pre_W = 0;
   // set (with canon_bits): the sort reads these raw u64 values (entries [0, n_u64)) instead
   const uint64_t *u64 = nullptr;
   size_t n_u64 = 0;
@@ -539,6 +542,11 @@ struct SortInput {
   bool mont = false;
   const uint64_t *u64 = nullptr;
   size_t n_u64 = 0;
+  // set: pass 1's tile histograms are already in the lane's count buffer (== precounted), computed
+  // for the shared-table plan (pre_c, pre_W) over these n scalars (quotient2_count_dev: the opening
+  // quotients' kernel counts their digits as it writes them); another plan recounts
+  const uint32_t *precounted = nullptr;
+  int pre_c = 0, pre_W = 0;
 };
 // A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
 // pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
@@ -568,6 +576,13 @@ void bucket_sort_passes(BucketSortJob &J);
 void bucket_sort_pass_rest(BucketSortJob &J, bool readback);
 BucketOrder bucket_sort_finish(BucketSortJob &J);
 // both phases at once (single MSMs)
+// The two opening MSMs' scalars q_k,i = (v_k - y_k,i) inv_i (canonical: the inverses are) with their
+// bit lengths, as lagrange_quotient_finish2_dev, AND pass 1's tile histograms of both sorts for the
+// shared-table plan (c, W) straight into lanes[0] / lanes[1]'s count buffers: the sorts skip their
+// count kernels (one read of both quotient vectors less).  false (nothing queued): no compile-time
+// pass-1 plan for (c, W) -- the caller runs the plain quotient kernel.
+bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr &v0, const Fr &v1, const Fr *inv,
+                         Fr *q0, Fr *q1, unsigned *bits, int cw, int W, const uint32_t *counts_out[2]);
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
@@ -676,6 +691,17 @@ struct HostTranscript {
   void append_fr(const Fr &x);
   Fr challenge(const char *label);
   Fr challenge_bytes(const uint8_t *label, size_t n);
+  // The next challenge's hash, started early: DefaultHasher writes the state's length FIRST, so no
+  // hash state carries over between challenges -- but once the length the state will have at the
+  // next challenge is known (a sum-check round appends fixed-size data), the SipHash blocks of the
+  // bytes already in the state can run while the device computes the round; challenge() then
+  // hashes only the round's own ~170 bytes.  Same hash, same challenge.
+  void prehash(size_t final_len);
+  struct Pre {
+    bool valid = false;
+    size_t final_len = 0, done = 0;  // bytes of the state absorbed (a multiple of 8)
+    uint64_t v[4];
+  } pre;
 };
 Fr commitment_hash(const G1Affine &a);
 Fr host_fr_rand_chacha(const uint8_t seed[32], uint8_t *fs_seed_out /* nullable: next 32 bytes */);

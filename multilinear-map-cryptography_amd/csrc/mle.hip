@@ -1058,6 +1058,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     Fr cur = claimed;
     char lab[64];
     uint32_t seq = queue(0);  // (nv == 0: the final kernel, reading the tables as they are)
+    if (nv > 0) tr.prehash(tr.state.size() + strlen("sumcheck_round_0") + 4 * 32 + strlen("sumcheck_challenge_0"));
     for (unsigned rnd = 0; rnd < nv; rnd++) {
       const uint32_t seq_next = queue(rnd + 1);
       Fr e[4];
@@ -1075,10 +1076,16 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       for (int x = 0; x < 4; x++) tr.append_fr(coeffs[x]);
       snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
       const Fr ch = tr.challenge(lab);
+      publish(rnd, ch);  // (first: the device's next round waits for it)
       if (challenges) challenges[rnd] = ch;
       cur = horner_host(coeffs, 4, ch);
-      publish(rnd, ch);
       seq = seq_next;
+      if (rnd + 1 < nv) {  // the next challenge's hash over the state so far, while the device works
+        char l1[64], l2[64];
+        const int n1 = snprintf(l1, sizeof l1, "sumcheck_round_%u", rnd + 1);
+        const int n2 = snprintf(l2, sizeof l2, "sumcheck_challenge_%u", rnd + 1);
+        tr.prehash(tr.state.size() + (size_t)n1 + 4 * 32 + (size_t)n2);
+      }
     }
     const ScResult &res = sc_wait(c, seq);
     Fr vals[MAX_SC_TABLES];

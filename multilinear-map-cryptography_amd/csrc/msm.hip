@@ -1104,6 +1104,9 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
       in.n_u64 = x.n_u64;
     } else {
       in.fr = x.canon ? x.canon : x.scalars;
+      in.precounted = x.precounted;
+      in.pre_c = x.pre_c;
+      in.pre_W = x.pre_W;
     }
     return in;
   };

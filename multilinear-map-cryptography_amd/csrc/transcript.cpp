@@ -40,20 +40,22 @@ void chacha20_block_host(const uint32_t key[8], uint64_t counter, uint32_t out[1
 }
 
 namespace {
-// rand_core BlockRng over ChaCha20 with a 4-block (64-word) buffer.
+// rand_core BlockRng over ChaCha20 (a 4-block buffer there: the word stream is blocks 0, 1, 2, ...
+// in order either way, so blocks are made one at a time here -- a challenge's Fr::rand reads 8
+// words, and the other three blocks were 0.6 us of every sum-check round's host turn)
 struct ChaChaStream {
   uint32_t key[8];
   uint64_t ctr = 0;
-  uint32_t buf[64];
-  int pos = 64;
+  uint32_t buf[16];
+  int pos = 16;
   explicit ChaChaStream(const uint8_t seed[32]) {
     for (int i = 0; i < 8; i++)
       key[i] = (uint32_t)seed[4 * i] | (uint32_t)seed[4 * i + 1] << 8 |
                (uint32_t)seed[4 * i + 2] << 16 | (uint32_t)seed[4 * i + 3] << 24;
   }
   uint32_t word() {
-    if (pos == 64) {
-      for (int b = 0; b < 4; b++) chacha20_block_host(key, ctr++, buf + 16 * b);
+    if (pos == 16) {
+      chacha20_block_host(key, ctr++, buf);
       pos = 0;
     }
     return buf[pos++];
@@ -105,8 +107,11 @@ void host_fr_rand_stream(const uint8_t seed[32], size_t n, Fr *out) {
 }
 
 // SipHash-1-3 with zero keys (Rust's DefaultHasher) over  prefix (8 bytes, if has_prefix) || m[0..n):
-// Hash for [u8] writes the length first, and the message is hashed in place (no concatenated copy)
-static uint64_t siphash13_keys00_pre(bool has_prefix, uint64_t prefix, const uint8_t *m, size_t n) {
+// Hash for [u8] writes the length first, and the message is hashed in place (no concatenated copy).
+// resume (optional): the state after the prefix and m's first `skip` bytes (skip % 8 == 0), from
+// HostTranscript::prehash -- only m[skip, n) is absorbed here.
+static uint64_t siphash13_keys00_pre(bool has_prefix, uint64_t prefix, const uint8_t *m, size_t n,
+                                     const uint64_t *resume = nullptr, size_t skip = 0, uint64_t *save = nullptr) {
   uint64_t v0 = 0x736f6d6570736575ULL, v1 = 0x646f72616e646f6dULL;
   uint64_t v2 = 0x6c7967656e657261ULL, v3 = 0x7465646279746573ULL;
   auto round = [&]() {
@@ -120,12 +125,27 @@ static uint64_t siphash13_keys00_pre(bool has_prefix, uint64_t prefix, const uin
     round();
     v0 ^= w;
   };
-  if (has_prefix) block(prefix);  // (8 bytes: a whole block, the message stays block-aligned)
   size_t i = 0;
+  if (resume) {
+    v0 = resume[0];
+    v1 = resume[1];
+    v2 = resume[2];
+    v3 = resume[3];
+    i = skip;
+  } else if (has_prefix) {
+    block(prefix);  // (8 bytes: a whole block, the message stays block-aligned)
+  }
   for (; i + 8 <= n; i += 8) {
     uint64_t w;
     std::memcpy(&w, m + i, 8);  // little-endian host
     block(w);
+  }
+  if (save) {  // (prehash: the whole blocks only, no finalisation)
+    save[0] = v0;
+    save[1] = v1;
+    save[2] = v2;
+    save[3] = v3;
+    return 0;
   }
   const size_t total = n + (has_prefix ? 8 : 0);
   uint64_t b = (uint64_t)(total & 0xff) << 56;
@@ -149,10 +169,23 @@ void HostTranscript::append_fr(const Fr &x) {
     for (int k = 0; k < 4; k++) b[4 * i + k] = (uint8_t)(c.v[i] >> (8 * k));
   append_bytes(b, 32);
 }
+void HostTranscript::prehash(size_t final_len) {
+  pre.valid = false;
+  if (final_len < state.size()) return;
+  const size_t whole = state.size() / 8 * 8;
+  siphash13_keys00_pre(true, (uint64_t)final_len, state.data(), whole, nullptr, 0, pre.v);
+  pre.final_len = final_len;
+  pre.done = whole;
+  pre.valid = true;
+}
 Fr HostTranscript::challenge_bytes(const uint8_t *label, size_t n) {
   append_bytes(label, n);
-  // Hash for [u8]: write_usize(len) first, then the bytes
-  const uint64_t h = siphash13_keys00_pre(true, (uint64_t)state.size(), state.data(), state.size());
+  // Hash for [u8]: write_usize(len) first, then the bytes (resumed after the prehashed blocks when
+  // the state reached the length prehash assumed)
+  const bool resume = pre.valid && pre.final_len == state.size() && pre.done <= state.size();
+  const uint64_t h = siphash13_keys00_pre(true, (uint64_t)state.size(), state.data(), state.size(),
+                                          resume ? pre.v : nullptr, resume ? pre.done : 0);
+  pre.valid = false;
   uint8_t seed[32];
   for (int k = 0; k < 4; k++) std::memcpy(seed + 8 * k, &h, 8);  // hash.to_le_bytes() x 4
   ChaChaStream g(seed);

@@ -1,6 +1,6 @@
 """bench.py's C2 and C3 extras alone (setup_params(18) + its 2^20 Lagrange basis, as the bench
 prepares them): KZG MSM of 2^20 Fr::rand scalars ([7;32]) and Shout::prove of the 2^20 squares
-table with 2^20 lookups; one JSON line.  For table-window A/Bs (TNS_TABLE_C=c).
+table with 2^20 lookups; one JSON line.
     python3 tools/c2c3_bench.py"""
 import json
 import os
@@ -29,7 +29,7 @@ n = 1 << 20
 pp18, _ = ts.setup_params(18)
 pp18.commitment_params.srs.prepare_lagrange(n)
 sc = ts.DeviceBuffer(ctx, ts.fr_rand_batch(bytes([7] * 32), n))
-out = {"table_c_env": os.environ.get("TNS_TABLE_C")}
+out = {}
 ref = ts.msm_resident(pp18.commitment_params, sc, n)
 out["msm_ms_2^20"] = round(timed(lambda: ts.msm_resident(pp18.commitment_params, sc, n), 20) * 1e3, 3)
 out["msm_commitment_hash"] = int(ref[0] ^ ref[4])
