@@ -291,6 +291,8 @@ struct Ctx {
   DevBuf sc_poly;                       // ... and its composition (ScPoly, mle.hip)
   PinnedBuf sc_poly_host;               // (its host staging copy)
   MappedHostBuf sc_mapped;              // sum-check round results + flag, polled by the host
+  MappedHostBuf inv_mapped;             // the batch inversion's grand product + flag (lagrange.hip)
+  uint32_t inv_seq = 0;
   uint32_t sc_seq = 0;                  // the flag value of the latest round launch
   MappedHostBuf sc_handoff;             // sum-check challenges for pre-queued round kernels (host writes)
   DevBuf sc_rdev;                       // ... each copied to device memory by the waiting kernel

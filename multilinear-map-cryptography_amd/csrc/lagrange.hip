@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "hostfield.hpp"
 
 namespace tns {
 
@@ -94,6 +95,110 @@ __global__ void __launch_bounds__(256) k_chain_inv(const Fr *__restrict__ cp, si
   __syncthreads();
   const Fr after = tid < 255 ? sh[tid + 1] : Fr::one();  // prod over s > t
   if (t < T) icp[t] = zero ? Fr::zero() : mul(mul(before, after), inv_total);
+}
+
+// The same batch inversion with ONE inverse for the whole grid, taken on the host: a single-lane
+// binary Euclid per block (k_chain_inv) is ~0.15-0.2 ms of dependent 256-bit steps on the
+// barycentric pass's critical path, the host's 4 x u64 inverse ~20 us.
+// (1) per block of 256 chains: icp[t] = the product of the block's OTHER chains, tot[b] = the block's
+//     product (zero chains count as one and are flagged: their inverse is 0);
+__global__ void __launch_bounds__(256) k_chain_local(const Fr *__restrict__ cp, size_t T, Fr *__restrict__ icp,
+                                                     Fr *__restrict__ tot) {
+  __shared__ Fr sh[256];
+  const int tid = threadIdx.x;
+  const size_t t = blockIdx.x * (size_t)blockDim.x + tid;
+  Fr a = t < T ? cp[t] : Fr::one();
+  const bool zero = a.is_zero();
+  if (zero) a = Fr::one();
+  Fr lo = a, hi = a;  // inclusive prefix / suffix products over the block
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = lo;
+    __syncthreads();
+    const Fr o = tid >= off ? sh[tid - off] : Fr::one();
+    __syncthreads();
+    lo = mul(o, lo);
+  }
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = hi;
+    __syncthreads();
+    const Fr o = tid + off < 256 ? sh[tid + off] : Fr::one();
+    __syncthreads();
+    hi = mul(hi, o);
+  }
+  if (tid == 0) tot[blockIdx.x] = hi;
+  sh[tid] = lo;
+  __syncthreads();
+  const Fr before = tid ? sh[tid - 1] : Fr::one();
+  __syncthreads();
+  sh[tid] = hi;
+  __syncthreads();
+  const Fr after = tid < 255 ? sh[tid + 1] : Fr::one();
+  if (t < T) icp[t] = zero ? Fr::zero() : mul(before, after);
+}
+
+// (2) one block over the nb <= 1024 block products: oth[b] = the product of the OTHER blocks, and the
+//     grand product to the host (mapped memory, then the flag)
+__global__ void __launch_bounds__(256) k_chain_totals(const Fr *__restrict__ tot, int nb, Fr *__restrict__ oth,
+                                                      Fr *pub, uint32_t *flag, uint32_t seq) {
+  __shared__ Fr sh[256];
+  constexpr int PER = 4;  // blocks per thread (nb <= 1024)
+  const int tid = threadIdx.x;
+  Fr v[PER], lo = Fr::one();
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int b = tid * PER + k;
+    v[k] = b < nb ? tot[b] : Fr::one();
+    lo = mul(lo, v[k]);
+  }
+  Fr hi = lo;
+  const Fr mine = lo;
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = lo;
+    __syncthreads();
+    const Fr o = tid >= off ? sh[tid - off] : Fr::one();
+    __syncthreads();
+    lo = mul(o, lo);
+  }
+  for (int off = 1; off < 256; off <<= 1) {
+    sh[tid] = hi;
+    __syncthreads();
+    const Fr o = tid + off < 256 ? sh[tid + off] : Fr::one();
+    __syncthreads();
+    hi = mul(hi, o);
+  }
+  sh[tid] = lo;
+  __syncthreads();
+  Fr before = tid ? sh[tid - 1] : Fr::one();  // blocks of the threads before this one
+  __syncthreads();
+  sh[tid] = hi;
+  __syncthreads();
+  const Fr after = tid < 255 ? sh[tid + 1] : Fr::one();
+  (void)mine;
+  // inside the thread: prefix and suffix over its PER blocks
+  Fr suf[PER];
+  suf[PER - 1] = Fr::one();
+#pragma unroll
+  for (int k = PER - 2; k >= 0; k--) suf[k] = mul(suf[k + 1], v[k + 1]);
+#pragma unroll
+  for (int k = 0; k < PER; k++) {
+    const int b = tid * PER + k;
+    if (b < nb) oth[b] = mul(mul(before, suf[k]), after);
+    before = mul(before, v[k]);
+  }
+  if (tid == 0) {
+    *pub = hi;  // thread 0's suffix = every block's product
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// (3) icp[t] *= oth[block of t] * inv_all (the host's inverse of the grand product, times scale)
+__global__ void __launch_bounds__(256) k_chain_apply(Fr *__restrict__ icp, size_t T, const Fr *__restrict__ oth,
+                                                     Fr inv_all) {
+  const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  const Fr o = mul(oth[blockIdx.x], inv_all);
+  icp[t] = mul(icp[t], o);  // (a flagged zero chain stays 0)
 }
 
 // out[blockIdx.x] = prod of in[i] over the block's grid-stride share (one level of a product tree)
@@ -324,10 +429,38 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   k_node_chain<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, n, s.T, s.Tm, skip, pre, s.cp);
   TNS_LAUNCH_CHECK();
   prod_reduce(c->stream, s.cp, s.T, s.dev + 4, s.dev);
-  // the chain products' inverses by one batch inversion per block of 256 chains
+  // the chain products' inverses: one batch inversion over all chains, its single inverse on the host
   s.inverted = true;
   s.icp = s.dev + 4 + 256;
-  k_chain_inv<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(s.cp, s.T, s.icp, scale);
+  const unsigned nb = grid_for(s.T, 256, 1u << 30);
+  Fr *tot = (Fr *)c->scratch[6].ensure(sizeof(Fr) * 2 * nb), *oth = tot + nb;
+  if (nb > 1024) {  // (more than 2^18 chains: one inverse per block, on the device)
+    k_chain_inv<<<nb, 256, 0, c->stream>>>(s.cp, s.T, s.icp, scale);
+    TNS_LAUNCH_CHECK();
+    return s;
+  }
+  k_chain_local<<<nb, 256, 0, c->stream>>>(s.cp, s.T, s.icp, tot);
+  TNS_LAUNCH_CHECK();
+  char *m = (char *)c->inv_mapped.ensure(64 + sizeof(Fr));
+  const uint32_t seq = ++c->inv_seq;
+  k_chain_totals<<<1, 256, 0, c->stream>>>(tot, (int)nb, oth, (Fr *)((char *)c->inv_mapped.dev + 64),
+                                           (uint32_t *)c->inv_mapped.dev, seq);
+  TNS_LAUNCH_CHECK();
+  const volatile uint32_t *flag = (const volatile uint32_t *)m;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1; __atomic_load_n((const uint32_t *)flag, __ATOMIC_ACQUIRE) != seq; spin++)
+    if ((spin & 4095) == 0) {  // a faulted stream reports here instead of leaving the flag unset
+      const hipError_t e = hipStreamQuery(c->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) TNS_HIP(e);
+      if (e == hipSuccess && __atomic_load_n((const uint32_t *)flag, __ATOMIC_ACQUIRE) != seq)
+        throw Error(TNS_ERR_DEVICE, "batch inversion: stream idle without its grand product");
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 120.0)
+        throw Error(TNS_ERR_DEVICE, "batch inversion: grand product did not arrive within 120 s");
+    }
+  Fr all;
+  std::memcpy(&all, m + 64, sizeof(Fr));
+  const Fr inv_all = mul(h_inv(HFr::of(all)).fp(), scale);  // (all != 0: zero chains count as one)
+  k_chain_apply<<<nb, 256, 0, c->stream>>>(s.icp, s.T, oth, inv_all);
   TNS_LAUNCH_CHECK();
   return s;
 }

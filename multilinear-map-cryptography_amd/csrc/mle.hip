@@ -892,7 +892,13 @@ static ScRun sc_run(Ctx *c, int k, const SumcheckTerm *terms, int n_terms, size_
 //  * the rounds of <= 2^SC_PTAIL_LOG pairs and the final fold run as one persistent launch of at
 //    most SC_PTAIL_BLOCKS one-wave blocks (k_sc_tail; 64 beat 16-1024);
 //  * each round's kernels are queued before its challenge exists (k_sc_wait_r).
-constexpr unsigned SC_SPLIT_LOG = 13, SC_PTAIL_LOG = 13, SC_PTAIL_BLOCKS = 64;
+#ifndef TNS_SC_SPLIT_LOG  // (build-time A/B only: tools/build_variant.sh)
+#define TNS_SC_SPLIT_LOG 13
+#endif
+#ifndef TNS_SC_PTAIL_LOG
+#define TNS_SC_PTAIL_LOG 13
+#endif
+constexpr unsigned SC_SPLIT_LOG = TNS_SC_SPLIT_LOG, SC_PTAIL_LOG = TNS_SC_PTAIL_LOG, SC_PTAIL_BLOCKS = 64;
 
 // one round's launch (tables already in kernel order); returns the flag value to wait for
 template <bool FOLD, bool SKIP1>
