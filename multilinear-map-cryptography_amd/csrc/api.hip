@@ -204,8 +204,7 @@ static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affin
                                   ExtraPayload *extra = nullptr) {
   const size_t xb = extra ? extra->bytes : 0;
   if (m.size == 1) {
-    out[0] = xyzz_to_affine(part[0]);
-    out[1] = xyzz_to_affine(part[1]);
+    xyzz_to_affine2(part[0], part[1], out[0], out[1]);
     if (xb) extra->all.assign((const uint8_t *)extra->data, (const uint8_t *)extra->data + xb);
     return;
   }
@@ -217,8 +216,8 @@ static void allgather_sum_g1_pair(Ctx *c, Comm &m, const G1Xyzz part[2], G1Affin
   mine[1] = part[1];
   if (xb) std::memcpy(&mine[2], extra->data, xb);
   m.exchange(c, mine.data(), rec, all.data(), what);
-  out[0] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, (int)recw, 0));
-  out[1] = xyzz_to_affine(sum_rank_parts(all.data(), m.size, (int)recw, 1));
+  xyzz_to_affine2(sum_rank_parts(all.data(), m.size, (int)recw, 0), sum_rank_parts(all.data(), m.size, (int)recw, 1),
+                  out[0], out[1]);
   if (xb) {
     extra->all.resize(xb * (size_t)m.size);
     for (int r = 0; r < m.size; r++)

@@ -744,19 +744,37 @@ TNS_HD G1Xyzz xyzz_mul_small(const G1Xyzz &p, u64 k) {
 }
 
 // XYZZ -> affine (one field inversion)
-TNS_HD G1Affine xyzz_to_affine(const G1Xyzz &p) {
+// p with 1/ZZZ already known
+TNS_HD G1Affine xyzz_to_affine_izzz(const G1Xyzz &p, const Fq &izzz) {
   G1Affine r;
-  if (p.is_inf()) {
-    r.x = Fq::zero();
-    r.y = Fq::zero();
-    return r;
-  }
-  Fq izzz = inv(p.zzz);         // 1/ZZZ
   Fq iz = mul(izzz, p.zz);      // ZZ/ZZZ = 1/z  (z = ZZZ/ZZ)
   Fq izz = sqr(iz);             // 1/ZZ
   r.x = mul(p.x, izz);
   r.y = mul(p.y, izzz);
   return r;
+}
+
+TNS_HD G1Affine xyzz_to_affine(const G1Xyzz &p) {
+  if (p.is_inf()) {
+    G1Affine r;
+    r.x = Fq::zero();
+    r.y = Fq::zero();
+    return r;
+  }
+  return xyzz_to_affine_izzz(p, inv(p.zzz));
+}
+
+// two points with ONE field inversion (Montgomery's trick): the host converts a proof's two
+// commitments / two opening proofs back to back on the critical path (~19 us an inversion)
+TNS_HD void xyzz_to_affine2(const G1Xyzz &p, const G1Xyzz &q, G1Affine &a, G1Affine &b) {
+  if (p.is_inf() || q.is_inf()) {
+    a = xyzz_to_affine(p);
+    b = xyzz_to_affine(q);
+    return;
+  }
+  const Fq it = inv(mul(p.zzz, q.zzz));
+  a = xyzz_to_affine_izzz(p, mul(it, q.zzz));
+  b = xyzz_to_affine_izzz(q, mul(it, p.zzz));
 }
 
 // affine -> arkworks G1Projective (Jacobian, Z = 1; identity = (1, 1, 0))

@@ -176,11 +176,21 @@ static_assert(BS_MAXBINS <= 2 * BS_BLOCK, "two bins per thread in the block scan
 // opening, their ~64-byte runs of half-dword stores costing more than the bytes saved.)
 enum { KF_U32 = 0, KF_U16 = 1 };
 
+// the scatters' stores (TNS_BS_NT build: non-temporal, A/B)
+template <class T>
+__device__ __forceinline__ void st_out(T *p, T v) {
+#if defined(TNS_BS_NT) && TNS_BS_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 __device__ __forceinline__ void store_entry(int kf, uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,
                                             uint32_t pos, uint32_t key, uint32_t val) {
-  if (kf == KF_U32) okeys[pos] = key;
-  else reinterpret_cast<uint16_t *>(okeys)[pos] = (uint16_t)key;
-  ovals[pos] = val;
+  if (kf == KF_U32) st_out(okeys + pos, key);
+  else st_out(reinterpret_cast<uint16_t *>(okeys) + pos, (uint16_t)key);
+  st_out(ovals + pos, val);
 }
 
 // entry i's key (the low bits a pass still needs) and value in format kf
@@ -574,11 +584,11 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter(PassGeom G, size_t S, c
     if (PK == 0) {
       store_entry(G.kout, okeys, ovals, pos, key, lv[slot]);
     } else if (PK == 3) {
-      ovals[pos] = lv[slot];
+      st_out(ovals + pos, lv[slot]);
     } else if (PK == 1) {
-      okeys[pos] = pack_entry(P, key, lv[slot]);
+      st_out(okeys + pos, pack_entry(P, key, lv[slot]));
     } else {
-      ovals[pos] = unpack_value(P, key);
+      st_out(ovals + pos, unpack_value(P, key));
     }
   }
 }
