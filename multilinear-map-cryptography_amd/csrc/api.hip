@@ -325,6 +325,7 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
     a1.precounted = pre[1];
     a0.pre_c = a1.pre_c = f0->c;
     a0.pre_W = a1.pre_W = f0->W;
+    a0.plan_bits = a1.plan_bits = 254;  // (the counts assumed the full-width table plan)
   }
   msm_pair_dev(c, a0, a1, pp);
   if (extra && extra_ready) extra_ready();

@@ -470,11 +470,100 @@ __device__ Fp<C> inv_binary_dev(const Fp<C> &a) {
 }
 #endif
 
-// Fermat inverse (a^(M-2)); inverse of zero is zero.
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host inverse by the binary extended Euclid on 4 x u64 limbs (~3x faster than the Fermat chain's
+// ~380 products: the host inverts on the proof's critical path -- the commitments' and openings'
+// affine forms, the barycentric batch inversion's one inverse).  a = xR (Montgomery limbs < M) ->
+// r = (xR)^-1 mod M, and x^-1 R = mont(r, R^3).  Inverse of zero is zero.
+template <class C>
+inline Fp<C> inv_binary_host(const Fp<C> &a) {
+  typedef unsigned __int128 u128;
+  u64 u[4], v[4], x1[4] = {1, 0, 0, 0}, x2[4] = {0, 0, 0, 0}, m[4];
+  for (int i = 0; i < 4; i++) {
+    u[i] = (u64)a.v[2 * i] | ((u64)a.v[2 * i + 1] << 32);
+    m[i] = (u64)C::M[2 * i] | ((u64)C::M[2 * i + 1] << 32);
+    v[i] = m[i];
+  }
+  auto is_one = [](const u64 *w) { return w[0] == 1 && (w[1] | w[2] | w[3]) == 0; };
+  auto shr1 = [](u64 *w) {
+    for (int i = 0; i < 3; i++) w[i] = (w[i] >> 1) | (w[i + 1] << 63);
+    w[3] >>= 1;
+  };
+  auto half_mod = [&](u64 *x) {  // x / 2 mod M (x < M < 2^255: x + M fits)
+    if (x[0] & 1) {
+      u64 c = 0;
+      for (int i = 0; i < 4; i++) {
+        const u128 t = (u128)x[i] + m[i] + c;
+        x[i] = (u64)t;
+        c = (u64)(t >> 64);
+      }
+    }
+    shr1(x);
+  };
+  auto geq = [](const u64 *p, const u64 *q) {
+    for (int i = 3; i >= 0; i--)
+      if (p[i] != q[i]) return p[i] > q[i];
+    return true;
+  };
+  auto sub_in = [](u64 *p, const u64 *q) {  // p -= q, returns the borrow
+    u64 b = 0;
+    for (int i = 0; i < 4; i++) {
+      const u128 t = (u128)p[i] - q[i] - b;
+      p[i] = (u64)t;
+      b = (u64)(t >> 64) & 1;
+    }
+    return b;
+  };
+  auto sub_mod = [&](u64 *p, const u64 *q) {  // p = p - q mod M
+    if (sub_in(p, q)) {
+      u64 c = 0;
+      for (int i = 0; i < 4; i++) {
+        const u128 t = (u128)p[i] + m[i] + c;
+        p[i] = (u64)t;
+        c = (u64)(t >> 64);
+      }
+    }
+  };
+  while (geq(u, m)) sub_in(u, m);  // (a lazily reduced input: < 2M)
+  if ((u[0] | u[1] | u[2] | u[3]) == 0) return Fp<C>::zero();
+  while (!is_one(u) && !is_one(v)) {
+    while ((u[0] & 1) == 0) {
+      shr1(u);
+      half_mod(x1);
+    }
+    while ((v[0] & 1) == 0) {
+      shr1(v);
+      half_mod(x2);
+    }
+    if (geq(u, v)) {
+      sub_in(u, v);
+      sub_mod(x1, x2);
+    } else {
+      sub_in(v, u);
+      sub_mod(x2, x1);
+    }
+  }
+  const u64 *r = is_one(u) ? x1 : x2;
+  Fp<C> out, r2;
+  for (int i = 0; i < 4; i++) {
+    out.v[2 * i] = (u32)r[i];
+    out.v[2 * i + 1] = (u32)(r[i] >> 32);
+  }
+  for (int i = 0; i < 8; i++) r2.v[i] = C::R2[i];
+  static const Fp<C> r3 = mul_cios64(r2, r2);  // R^3 mod M
+  return mul_cios64(out, r3);
+}
+#endif
+
+// Fermat inverse (a^(M-2)) on the device; the binary extended Euclid on the host.  Inverse of
+// zero is zero.
 template <class C>
 TNS_HD Fp<C> inv(const Fp<C> &a) {
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(TNS_MUL_CIOS)
   return inv_window_dev(a);
+#endif
+#if !defined(__HIP_DEVICE_COMPILE__)
+  return inv_binary_host(a);
 #endif
   u32 e[8];
   u64 br = 2;

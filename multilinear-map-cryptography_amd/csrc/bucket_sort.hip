@@ -292,13 +292,16 @@ __device__ __forceinline__ void scalar_digits_ct(const Fr &k, const DigitArgs &A
   }
 }
 
+// bits (optional): also the largest bit length of the (canonical) scalars -- the MSM's plan input,
+// computed here when the plan was known ahead (bucket_sort_precount_bits) instead of by k_scalar_bits
 template <int C, int W>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shift, int nbins, size_t T1,
-                                                           uint32_t *__restrict__ counts) {
+                                                           uint32_t *__restrict__ counts, unsigned *bits) {
   __shared__ uint32_t h[BS_MAXBINS];
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h[d] = 0;
   __syncthreads();
   const size_t tile = blockIdx.x, a = tile * A.spb, b = min(A.n, a + A.spb);
+  unsigned bl = 0;
   for (size_t i0 = a + threadIdx.x; i0 < b; i0 += (size_t)BS_SCALARS * BS_BLOCK) {
     Fr s[BS_SCALARS];  // the loads in flight together, then the digits
 #pragma unroll
@@ -306,12 +309,15 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shif
       if (i0 + (size_t)j * BS_BLOCK < b) s[j] = load_scalar(A, i0 + (size_t)j * BS_BLOCK);
 #pragma unroll
     for (int j = 0; j < BS_SCALARS; j++)
-      if (i0 + (size_t)j * BS_BLOCK < b)
+      if (i0 + (size_t)j * BS_BLOCK < b) {
+        if (bits) bl = max(bl, fr_bit_length(s[j]));
         scalar_digits_ct<C, W>(s[j], A, [&](int, uint32_t key, bool) { atomicAdd(&h[key >> shift], 1u); });
+      }
   }
   __syncthreads();
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) counts[(size_t)d * T1 + tile] = h[d];
   if (tile == 0 && threadIdx.x == 0) counts[(size_t)nbins * T1] = 0;
+  if (bits) block_atomic_max2(bl, 0u, bits, nullptr);
 }
 
 constexpr uint32_t BS_NOKEY = 0x40000000u;  // empty entry slot (keys are < 2^30; bit 31 = sign)
@@ -374,7 +380,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
 // the narrow trace commitments' per-window plans; anything else takes the runtime kernels
 struct Pass1Plan {
   int tile, c, W;
-  void (*count)(DigitArgs, int, int, size_t, uint32_t *);
+  void (*count)(DigitArgs, int, int, size_t, uint32_t *, unsigned *);
   void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, int, uint32_t *, uint32_t *);
   int spt;
 };
@@ -939,12 +945,12 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   const size_t tmin = 4096;  // the smallest pass tile
   const size_t max_tiles = (E + tmin - 1) / tmin + (max_seg >> bits[npass - 1]) + 1;
   const size_t cnt_len = std::max((size_t)nb * T1, (size_t)BS_MAXBINS * max_tiles) + 1;
-  const bool pre = in.precounted && shared && ct && in.pre_c == c && in.pre_W == W && ln.ws[12].p == in.precounted &&
-                   ln.ws[12].bytes >= sizeof(uint32_t) * cnt_len;
+  const bool pre = in.precounted && ct && in.pre_shared == shared && in.pre_c == c && in.pre_W == W &&
+                   ln.ws[12].p == in.precounted && ln.ws[12].bytes >= sizeof(uint32_t) * cnt_len;
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   if (!pre) {  // (precounted: quotient2_count_dev wrote them)
-    if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
+    if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts, nullptr);
     else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
     TNS_LAUNCH_CHECK();
   }
@@ -1144,6 +1150,21 @@ bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr 
   TNS_LAUNCH_CHECK();
   counts_out[0] = cnt[0];
   counts_out[1] = cnt[1];
+  return true;
+}
+
+bool bucket_sort_precount_bits(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, int bucket_bits,
+                               unsigned *bits, SortInput &in) {
+  const Pass1Geom g = pass1_geom(n, c, W, shared, bucket_bits);
+  if (!g.ct) return false;
+  uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * g.cnt_len);
+  DigitArgs A{scalars, n, g.spb, c, W, g.wb, shared, 0u, true, nullptr, 0};
+  g.ct->count<<<(unsigned)g.T1, BS_BLOCK, 0, ln.stream>>>(A, g.shift, g.nb, g.T1, counts, bits);
+  TNS_LAUNCH_CHECK();
+  in.precounted = counts;
+  in.pre_c = c;
+  in.pre_W = W;
+  in.pre_shared = shared;
   return true;
 }
 

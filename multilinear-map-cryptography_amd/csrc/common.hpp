@@ -137,6 +137,14 @@ struct MsmLane {
   // tile totals, 2 the MSM's per-set sums
   MappedHostBuf mapped;
   uint32_t pub_seq = 0;
+  // the window plan this lane's last MSM of Montgomery scalars took (n, c, W, layout): the next
+  // such MSM of n scalars counts pass 1 for it while it computes the scalars' bit length, and the
+  // sort uses those counts when the bit length confirms the plan (bucket_sort_precount_bits)
+  struct PlanHint {
+    size_t n = 0;
+    int c = 0, W = 0, bucket_bits = 0;
+    bool shared = false;
+  } hint;
   uint32_t slot_seq[3] = {0, 0, 0};
 };
 // (msm.hip) readbacks through MsmLane::mapped: parts (device pointer, bytes; bytes % 4 == 0) are
@@ -499,6 +507,10 @@ struct MsmArgs {
   // set (with canon_bits, canonical scalars): pass 1's histograms are precounted (SortInput::precounted)
   const uint32_t *precounted = nullptr;
   int pre_c = 0, pre_W = 0;
+  // > 0: plan the MSM for scalars of this bit length without reading canon_bits back (the opening
+  // quotients: full width -- the table plan's extra windows of a narrower quotient carry no digits,
+  // so the entries are the same); the sort can be queued right behind the kernel writing the scalars
+  int plan_bits = 0;
   // set (with canon_bits): the sort reads these raw u64 values (entries [0, n_u64)) instead
   const uint64_t *u64 = nullptr;
   size_t n_u64 = 0;
@@ -549,6 +561,7 @@ struct SortInput {
   // quotients' kernel counts their digits as it writes them); another plan recounts
   const uint32_t *precounted = nullptr;
   int pre_c = 0, pre_W = 0;
+  bool pre_shared = true;
 };
 // A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
 // pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
@@ -585,6 +598,11 @@ BucketOrder bucket_sort_finish(BucketSortJob &J);
 // pass-1 plan for (c, W) -- the caller runs the plain quotient kernel.
 bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr &v0, const Fr &v1, const Fr *inv,
                          Fr *q0, Fr *q1, unsigned *bits, int cw, int W, const uint32_t *counts_out[2]);
+// n Montgomery scalars' largest bit length (into *bits, zeroed by the caller) together with pass 1's
+// histograms for the plan (c, W, shared, bucket_bits) in the lane's count buffer; `in` then carries
+// them as precounted.  false (nothing queued): no compile-time pass-1 plan for it.
+bool bucket_sort_precount_bits(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, int bucket_bits,
+                               unsigned *bits, SortInput &in);
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);
