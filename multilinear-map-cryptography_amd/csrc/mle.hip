@@ -578,6 +578,14 @@ __device__ bool sc_poll_host(ScChal *chal, uint32_t seq, Fr &r, ScResult *res) {
   return true;
 }
 
+// TNS_SC_TRACE builds (diagnostics, tools/sc_trace.py): the persistent tail records, per round, when
+// block 0 starts waiting for the challenge, when it has it and when the last block publishes the
+// round's sums (s_memrealtime, 100 MHz) into mapped host memory; the host adds its own turn times
+#ifndef TNS_SC_TRACE
+#define TNS_SC_TRACE 0
+#endif
+__device__ uint64_t *g_sc_trace = nullptr;
+
 template <int K>
 __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restrict__ qp, unsigned r0, unsigned nv,
                                                 size_t n, ScChal *chal, uint32_t chal_base, ScResult *res,
@@ -595,7 +603,13 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
       bool ok = true;
       Fr r;
       if (blockIdx.x == 0) {
+#if TNS_SC_TRACE
+        if (g_sc_trace) g_sc_trace[4 * t] = __builtin_amdgcn_s_memrealtime();
+#endif
         ok = sc_poll_host(chal, chal_base + rr, r, res);
+#if TNS_SC_TRACE
+        if (g_sc_trace) g_sc_trace[4 * t + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (ok) {
           sync->r[t] = r;
           __hip_atomic_store(&sync->rflag, t + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -646,6 +660,9 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
     const size_t P = n >> (rr + 1);
     const Fr acc = sc_split_sweep<true, K, true>(tt, q, P, r, blockIdx.x, gridDim.x);
     sc_split_finish(acc, partials, counter, res, seq_base + t, lds, &last);
+#if TNS_SC_TRACE
+    if (last && threadIdx.x == 0 && g_sc_trace) g_sc_trace[4 * t + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();  // (ok_s / r_s are rewritten by thread 0 next round)
   }
 }
@@ -1060,6 +1077,16 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     R.chal->r = ch;
     __atomic_store_n(&R.chal->flag, chal_base + i + 1, __ATOMIC_RELEASE);
   };
+#if TNS_SC_TRACE
+  static MappedHostBuf trace_buf;
+  uint64_t *trace_h = (uint64_t *)trace_buf.ensure(4 * 64 * sizeof(uint64_t));
+  std::memset(trace_h, 0, 4 * 64 * sizeof(uint64_t));
+  uint64_t *trace_d = (uint64_t *)trace_buf.dev;
+  TNS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_sc_trace), &trace_d, sizeof trace_d, 0, hipMemcpyHostToDevice, c->stream));
+  std::vector<double> t_seen(nv + 1, 0.0), t_pub(nv + 1, 0.0);
+  const auto tt0 = std::chrono::steady_clock::now();
+  auto us = [&]() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tt0).count(); };
+#endif
   try {
     Fr cur = claimed;
     char lab[64];
@@ -1069,6 +1096,9 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       const uint32_t seq_next = queue(rnd + 1);
       Fr e[4];
       sc_round_sums(R, seq, e);
+#if TNS_SC_TRACE
+      t_seen[rnd] = us();
+#endif
       if (rnd > 0) e[1] = sub(cur, e[0]);  // (SKIP1 rounds; round 0 forms g(1) and checks the claim)
       Fr coeffs[4];
       interpolate4_host(e, coeffs);  // lagrange_interpolate of 4 points (src/sumcheck.rs:201-206)
@@ -1083,6 +1113,9 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
       const Fr ch = tr.challenge(lab);
       publish(rnd, ch);  // (first: the device's next round waits for it)
+#if TNS_SC_TRACE
+      t_pub[rnd] = us();
+#endif
       if (challenges) challenges[rnd] = ch;
       cur = horner_host(coeffs, 4, ch);
       seq = seq_next;
@@ -1094,6 +1127,22 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       }
     }
     const ScResult &res = sc_wait(c, seq);
+#if TNS_SC_TRACE
+    t_seen[nv] = us();
+    for (unsigned rnd = 0; rnd < nv; rnd++)
+      fprintf(stderr, "[sc-trace] round %2u host: sums seen %9.1f us, challenge out %9.1f us (turn %5.1f us)%s\n", rnd,
+              t_seen[rnd], t_pub[rnd], t_pub[rnd] - t_seen[rnd], rnd >= r0 ? " [tail]" : "");
+    fprintf(stderr, "[sc-trace] final seen %9.1f us\n", t_seen[nv]);
+    for (unsigned t = 0; tail && r0 + t < nv; t++) {
+      const uint64_t *d = trace_h + 4 * t, *dn = trace_h + 4 * (t + 1);
+      const double wait = (d[1] - d[0]) * 0.01, comp = (d[2] - d[1]) * 0.01;
+      const double turn = (r0 + t + 1 < nv && dn[1]) ? (dn[1] - d[2]) * 0.01 : -1;
+      fprintf(stderr, "[sc-trace] tail round %2u (pairs %zu): device wait for r %7.1f us, compute+publish %7.1f us, "
+                      "publish -> next r on device %7.1f us\n", r0 + t, n >> (r0 + t + 1), wait, comp, turn);
+    }
+    void *nullp = nullptr;
+    TNS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sc_trace), &nullp, sizeof nullp));
+#endif
     Fr vals[MAX_SC_TABLES];
     for (int m = 0; m < k; m++) vals[R.perm[m]] = res.sums[m];
     for (int i = 0; i < k; i++) final_vals[i] = vals[i];

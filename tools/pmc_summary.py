@@ -14,12 +14,13 @@ import json
 import sys
 
 STAGES = {
-    "msm_digits": (["k_digits", "k_scalar_bits", "k_u64_tables"], 2),  # the commitments (openings arrive canonical)
-    "msm_sort": (["rocprim", "k_bucket_bounds", "k_bs_"], 4),
+    "msm_digits": (["k_scalar_bits", "k_u64_tables"], 2),  # the commitments (openings arrive canonical)
+    "msm_sort": (["k_bs_", "k_scan_"], 4),
     "msm_accumulate": (["k_accumulate"], 4),
     "msm_fixup": (["k_fix_level", "k_bucket_fixup"], 4),
     "msm_reduce": (["k_reduce_level", "k_masked_sums", "k_sum_chunks", "k_set_sum"], 4),
-    "open_scan": (["k_node_chain", "k_prod_reduce", "k_node_finish", "k_sum_reduce", "k_node_quotient"], 2),
+    "open_scan": (["k_node_chain", "k_prod_reduce", "k_chain_", "k_node_finish", "k_sum_reduce", "k_node_quotient",
+                   "k_quotient2"], 2),
     "sumcheck_round": (["k_sc_round", "k_sc_fold3", "k_sc_fold_tail", "k_sum_partials4"], None),
 }
 
@@ -39,8 +40,16 @@ def per_kernel_last_step(path, counter, steps_total):
 
 def main():
     d, steps_total = sys.argv[1], int(sys.argv[2])
-    f = per_kernel_last_step(f"{d}/fetch/run_counter_collection.csv", "FETCH_SIZE", steps_total)
-    w = per_kernel_last_step(f"{d}/write/run_counter_collection.csv", "WRITE_SIZE", steps_total)
+    import glob
+
+    def find(sub):  # rocprofv3 may nest its output under host / pid directories
+        hits = sorted(glob.glob(f"{d}/{sub}/**/run_counter_collection.csv", recursive=True))
+        if not hits:
+            raise SystemExit(f"no run_counter_collection.csv under {d}/{sub}")
+        return hits[0]
+
+    f = per_kernel_last_step(find("fetch"), "FETCH_SIZE", steps_total)
+    w = per_kernel_last_step(find("write"), "WRITE_SIZE", steps_total)
     res = {"_note": "KiB counters x1024; FETCH_SIZE x2 (gfx950 correction, MI355X_MICROARCH.md HBM); "
                     "per stage launch, one bench step (last of the run)"}
     for st, (pats, launches) in STAGES.items():
