@@ -294,9 +294,11 @@ __device__ __forceinline__ void scalar_digits_ct(const Fr &k, const DigitArgs &A
 
 // bits (optional): also the largest bit length of the (canonical) scalars -- the MSM's plan input,
 // computed here when the plan was known ahead (bucket_sort_precount_bits) instead of by k_scalar_bits
+// low64 (optional, with bits): each scalar's canonical low 64 bits (the sort's narrow input, below)
 template <int C, int W>
 __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shift, int nbins, size_t T1,
-                                                           uint32_t *__restrict__ counts, unsigned *bits) {
+                                                           uint32_t *__restrict__ counts, unsigned *bits,
+                                                           uint64_t *__restrict__ low64) {
   __shared__ uint32_t h[BS_MAXBINS];
   for (int d = threadIdx.x; d < nbins; d += BS_BLOCK) h[d] = 0;
   __syncthreads();
@@ -311,6 +313,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_count1_ct(DigitArgs A, int shif
     for (int j = 0; j < BS_SCALARS; j++)
       if (i0 + (size_t)j * BS_BLOCK < b) {
         if (bits) bl = max(bl, fr_bit_length(s[j]));
+        if (low64) low64[i0 + (size_t)j * BS_BLOCK] = (uint64_t)s[j].v[0] | ((uint64_t)s[j].v[1] << 32);
         scalar_digits_ct<C, W>(s[j], A, [&](int, uint32_t key, bool) { atomicAdd(&h[key >> shift], 1u); });
       }
   }
@@ -380,7 +383,7 @@ __global__ void __launch_bounds__(BS_BLOCK) k_bs_scatter1_ct(DigitArgs A, int sh
 // the narrow trace commitments' per-window plans; anything else takes the runtime kernels
 struct Pass1Plan {
   int tile, c, W;
-  void (*count)(DigitArgs, int, int, size_t, uint32_t *, unsigned *);
+  void (*count)(DigitArgs, int, int, size_t, uint32_t *, unsigned *, uint64_t *);
   void (*scatter)(DigitArgs, int, int, size_t, const uint32_t *, int, uint32_t *, uint32_t *);
   int spt;
 };
@@ -950,7 +953,7 @@ void bucket_sort_begin(MsmLane &ln, const SortInput &in, size_t n, int c, int W,
   uint32_t *counts = J.counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * cnt_len);
   uint32_t *offs = J.offs = (uint32_t *)ln.ws[13].ensure(sizeof(uint32_t) * cnt_len);
   if (!pre) {  // (precounted: quotient2_count_dev wrote them)
-    if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts, nullptr);
+    if (ct) ct->count<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts, nullptr, nullptr);
     else k_bs_count1<<<(unsigned)T1, BS_BLOCK, 0, st>>>(A, shift, nb, T1, counts);
     TNS_LAUNCH_CHECK();
   }
@@ -1154,13 +1157,15 @@ bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr 
 }
 
 bool bucket_sort_precount_bits(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, int bucket_bits,
-                               unsigned *bits, SortInput &in) {
+                               unsigned *bits, SortInput &in, bool want_low64) {
   const Pass1Geom g = pass1_geom(n, c, W, shared, bucket_bits);
   if (!g.ct) return false;
   uint32_t *counts = (uint32_t *)ln.ws[12].ensure(sizeof(uint32_t) * g.cnt_len);
+  uint64_t *low = want_low64 ? (uint64_t *)ln.ws[18].ensure(sizeof(uint64_t) * n) : nullptr;
   DigitArgs A{scalars, n, g.spb, c, W, g.wb, shared, 0u, true, nullptr, 0};
-  g.ct->count<<<(unsigned)g.T1, BS_BLOCK, 0, ln.stream>>>(A, g.shift, g.nb, g.T1, counts, bits);
+  g.ct->count<<<(unsigned)g.T1, BS_BLOCK, 0, ln.stream>>>(A, g.shift, g.nb, g.T1, counts, bits, low);
   TNS_LAUNCH_CHECK();
+  in.low64 = low;
   in.precounted = counts;
   in.pre_c = c;
   in.pre_W = W;

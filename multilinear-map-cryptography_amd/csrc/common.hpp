@@ -129,7 +129,7 @@ struct MappedHostBuf {
 // (the two commitments, the two opening quotients) overlap on the device.
 struct MsmLane {
   hipStream_t stream = nullptr;
-  DevBuf ws[18];
+  DevBuf ws[19];
   DevBuf fix;       // heavy-bucket level sums
   // the lane's host readbacks without a stream synchronize: a one-block kernel copies the words
   // into this fine-grained host buffer and then sets the slot's flag, which the host polls
@@ -299,6 +299,7 @@ struct Ctx {
   DevBuf sc_poly;                       // ... and its composition (ScPoly, mle.hip)
   PinnedBuf sc_poly_host;               // (its host staging copy)
   MappedHostBuf sc_mapped;              // sum-check round results + flag, polled by the host
+  MappedHostBuf sc_htab;                // sum-check: the folded tables of the host's last rounds
   MappedHostBuf inv_mapped;             // the batch inversion's grand product + flag (lagrange.hip)
   uint32_t inv_seq = 0;
   uint32_t sc_seq = 0;                  // the flag value of the latest round launch
@@ -562,6 +563,10 @@ struct SortInput {
   const uint32_t *precounted = nullptr;
   int pre_c = 0, pre_W = 0;
   bool pre_shared = true;
+  // set (with precounted, Montgomery scalars): the count kernel also wrote each scalar's canonical
+  // low 64 bits here; when the bit length shows the scalars fit 64 bits the sort reads these
+  // (8 bytes a scalar, no Montgomery reduction) instead of the 32-byte scalars
+  const uint64_t *low64 = nullptr;
 };
 // A sort in flight: bucket_sort_begin (pass 1), bucket_sort_passes (the passes up to the last
 // pass's tile-total readback), bucket_sort_finish (waits for that readback, queues the rest);
@@ -602,7 +607,7 @@ bool quotient2_count_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t n, const Fr 
 // histograms for the plan (c, W, shared, bucket_bits) in the lane's count buffer; `in` then carries
 // them as precounted.  false (nothing queued): no compile-time pass-1 plan for it.
 bool bucket_sort_precount_bits(MsmLane &ln, const Fr *scalars, size_t n, int c, int W, bool shared, int bucket_bits,
-                               unsigned *bits, SortInput &in);
+                               unsigned *bits, SortInput &in, bool want_low64);
 BucketOrder bucket_sort_dev(MsmLane &ln, const SortInput &in, size_t n, int c, int W, bool shared, uint32_t stride,
                             int bucket_bits, uint32_t *valid);
 FixedBase *fixed_base_build_dev(Ctx *c, const G1Affine *points, size_t n);

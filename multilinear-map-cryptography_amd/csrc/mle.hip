@@ -16,6 +16,7 @@
 #include <cstring>
 
 #include "common.hpp"
+#include "hostfield.hpp"
 
 namespace tns {
 
@@ -578,6 +579,24 @@ __device__ bool sc_poll_host(ScChal *chal, uint32_t seq, Fr &r, ScResult *res) {
   return true;
 }
 
+// Rounds of <= SC_SOLO_PAIRS pairs run on block 0 alone: the grid-wide handoff of a round (the
+// challenge relayed through device memory, every block's partials, the last-block count) costs a
+// fixed ~13 us whatever the round's size (TNS_SC_TRACE, profiles/r06_sc_tail_trace.txt), while one
+// wave sweeps 64 pairs in ~4 passes.
+#ifndef TNS_SC_SOLO_PAIRS
+#define TNS_SC_SOLO_PAIRS 64
+#endif
+constexpr size_t SC_SOLO_PAIRS = TNS_SC_SOLO_PAIRS;
+
+// The last rounds, from the first of <= SC_HOST_PAIRS pairs, run on the host: the tail folds the
+// tables once more (by that round's r) into mapped host memory and ends, and the host sweeps the
+// few remaining pairs (4 x u64 arithmetic, hostfield.hpp) between its own transcript steps instead
+// of a device round trip per round (~13 us each, profiles/r06_sc_tail_trace.txt).  0 disables.
+#ifndef TNS_SC_HOST_PAIRS
+#define TNS_SC_HOST_PAIRS 64
+#endif
+constexpr size_t SC_HOST_PAIRS = TNS_SC_HOST_PAIRS;  // (the hand-over round runs on block 0 alone)
+
 // TNS_SC_TRACE builds (diagnostics, tools/sc_trace.py): the persistent tail records, per round, when
 // block 0 starts waiting for the challenge, when it has it and when the last block publishes the
 // round's sums (s_memrealtime, 100 MHz) into mapped host memory; the host adds its own turn times
@@ -590,7 +609,7 @@ template <int K>
 __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restrict__ qp, unsigned r0, unsigned nv,
                                                 size_t n, ScChal *chal, uint32_t chal_base, ScResult *res,
                                                 uint32_t seq_base, Fr *__restrict__ partials, unsigned *counter,
-                                                ScTailSync *sync) {
+                                                ScTailSync *sync, unsigned rh, Fr *__restrict__ htab) {
   __shared__ Fr lds[4 * 16];
   __shared__ int last;
   __shared__ Fr r_s;
@@ -598,7 +617,8 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
   const ScPoly &q = *qp;
   for (unsigned rr = r0; rr <= nv; rr++) {
     const unsigned t = rr - r0;
-    if (rr == nv && blockIdx.x != 0) return;  // (the final fold is block 0's)
+    const bool solo = rr >= rh || (n >> (rr + 1)) <= SC_SOLO_PAIRS;
+    if (solo && blockIdx.x != 0) return;  // (the final fold / hand-over and the smallest rounds are block 0's)
     if (threadIdx.x == 0) {  // r_{rr - 1}
       bool ok = true;
       Fr r;
@@ -641,6 +661,21 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
       tt.in[m] = rr % 2 == 0 ? pp.B[m] : pp.C[m];
       tt.out[m] = rr % 2 == 0 ? pp.C[m] : pp.B[m];
     }
+    if (rr == rh && rh < nv) {  // hand-over: the tables folded by r_{rh-1} (K x L, kernel order) to the host
+      const size_t L = n >> rr;
+#pragma unroll
+      for (int m = 0; m < K; m++) {
+        const Fr *p = tt.in[m];
+        for (size_t s = threadIdx.x; s < L; s += 64) {
+          const Fr p0 = sc_canon(p[2 * s]), p1 = sc_canon(p[2 * s + 1]);
+          htab[(size_t)m * L + s] = add(p0, mul(r, sub(p1, p0)));
+        }
+      }
+      __threadfence_system();
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(&res->flag, seq_base + t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     if (rr == nv) {  // the final fold: in holds the last round's 2-entry tables
       if (blockIdx.x == 0) {
         if (threadIdx.x < (unsigned)K) {
@@ -658,6 +693,18 @@ __global__ void __launch_bounds__(64) k_sc_tail(ScPing pp, const ScPoly *__restr
       return;
     }
     const size_t P = n >> (rr + 1);
+    if (solo) {  // block 0 sweeps every pair and publishes its own four sums
+      const Fr acc = sc_split_sweep<true, K, true>(tt, q, P, r, 0, 1);
+      if (threadIdx.x < 4) res->sums[threadIdx.x] = acc;
+      __threadfence_system();  // (also this round's table writes, read by other lanes next round)
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(&res->flag, seq_base + t, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#if TNS_SC_TRACE
+      if (threadIdx.x == 0 && g_sc_trace) g_sc_trace[4 * t + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
+      __syncthreads();
+      continue;
+    }
     const Fr acc = sc_split_sweep<true, K, true>(tt, q, P, r, blockIdx.x, gridDim.x);
     sc_split_finish(acc, partials, counter, res, seq_base + t, lds, &last);
 #if TNS_SC_TRACE
@@ -972,6 +1019,72 @@ static Fr eval_composition_host(const Fr *vals, const SumcheckTerm *terms, int n
   return s;
 }
 
+// The sum-check's last rounds on the host (SC_HOST_PAIRS): the same sums as the device's round
+// kernels -- g(X) = sum over pairs s of the composition at T[2s] + X (T[2s+1] - T[2s]), at X = 0, 2,
+// 3 (g(1) is the claim minus g(0)) -- and the same fold T'[s] = T[2s] + r (T[2s+1] - T[2s])
+// (src/sumcheck.rs:60-100), over tables in the caller's order
+struct ScHostRounds {
+  std::vector<HFr> t[MAX_SC_TABLES];
+  struct Term {
+    HFr coeff;
+    int tab[3];
+  };
+  std::vector<Term> terms;
+  int k = 0;
+  void load(const Fr *src, int k_, size_t L, const int *perm, const SumcheckTerm *tm, int n_terms) {
+    k = k_;
+    for (int m = 0; m < k; m++) {  // (kernel table m is the caller's perm[m])
+      std::vector<HFr> &v = t[perm[m]];
+      v.resize(L);
+      std::memcpy((void *)v.data(), (const void *)(src + (size_t)m * L), sizeof(Fr) * L);
+    }
+    terms.resize(n_terms);
+    for (int i = 0; i < n_terms; i++) {
+      terms[i].coeff = HFr::of(tm[i].coeff);
+      for (int j = 0; j < 3; j++) terms[i].tab[j] = tm[i].tab[j];
+    }
+  }
+  HFr comp(const HFr *v) const {
+    HFr s = HFr::zero();
+    for (const Term &tm : terms) {
+      HFr p = tm.coeff;
+      for (int j = 0; j < 3; j++)
+        if (tm.tab[j] >= 0) p = p * v[tm.tab[j]];
+      s = s + p;
+    }
+    return s;
+  }
+  void sums(Fr e[4]) const {
+    const size_t P = t[0].size() / 2;
+    HFr acc[3] = {HFr::zero(), HFr::zero(), HFr::zero()};
+    for (size_t s = 0; s < P; s++) {
+      HFr v[MAX_SC_TABLES], d[MAX_SC_TABLES];
+      for (int i = 0; i < k; i++) {
+        v[i] = t[i][2 * s];
+        d[i] = t[i][2 * s + 1] - v[i];
+      }
+      acc[0] = acc[0] + comp(v);
+      for (int x = 1; x < 3; x++) {  // X = 2, 3
+        for (int i = 0; i < k; i++) v[i] = v[i] + (x == 1 ? h_dbl(d[i]) : d[i]);
+        acc[x] = acc[x] + comp(v);
+      }
+    }
+    e[0] = acc[0].fp();
+    e[1] = Fr::zero();  // (the caller's: the claim minus g(0))
+    e[2] = acc[1].fp();
+    e[3] = acc[2].fp();
+  }
+  void fold(const Fr &r) {
+    const HFr hr = HFr::of(r);
+    for (int i = 0; i < k; i++) {
+      std::vector<HFr> &v = t[i];
+      const size_t h = v.size() / 2;
+      for (size_t s = 0; s < h; s++) v[s] = v[2 * s] + hr * (v[2 * s + 1] - v[2 * s]);
+      v.resize(h);
+    }
+  }
+};
+
 // sum over {0,1}^nv of the composition (the honest prover's claimed sum): round 0's sums at
 // X = 0 and X = 1, added
 Fr composition_sum_dev(Ctx *c, Fr *const *tables, int k, unsigned nv, const SumcheckTerm *terms, int n_terms) {
@@ -1023,6 +1136,18 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       break;
     }
   const bool tail = r0 < nv;
+  // the host's rounds: rh .. nv - 1 (rh == nv: none; the tail's final fold gives the values)
+  unsigned rh = nv;
+  for (unsigned rr = r0; tail && rr < nv; rr++)
+    if ((n >> (rr + 1)) <= SC_HOST_PAIRS) {
+      rh = rr;
+      break;
+    }
+  Fr *htab_dev = nullptr;
+  if (rh < nv) {
+    c->sc_htab.ensure(sizeof(Fr) * k * (n >> rh));
+    htab_dev = (Fr *)c->sc_htab.dev;
+  }
   uint32_t tail_seq = 0;
   // queue round rr (rr >= 1: behind the wait for challenge r_{rr-1}); rr == nv: the final fold
   auto queue = [&](unsigned rr) -> uint32_t {
@@ -1040,7 +1165,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
         const unsigned g = (unsigned)std::min<size_t>(SC_PTAIL_BLOCKS, std::max<size_t>(1, (n >> (r0 + 1)) / 16));
 #define TNS_SC_K(K)                                                                                             \
   k_sc_tail<K><<<g, 64, 0, c->stream>>>(pp, R.q_dev, r0, nv, n, R.chal_dev, chal_base, R.res_dev, tail_seq, \
-                                       R.partials, R.counter, sync)
+                                       R.partials, R.counter, sync, rh, htab_dev)
         switch (k) {
           case 1: TNS_SC_K(1); break;
           case 2: TNS_SC_K(2); break;
@@ -1092,10 +1217,19 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     char lab[64];
     uint32_t seq = queue(0);  // (nv == 0: the final kernel, reading the tables as they are)
     if (nv > 0) tr.prehash(tr.state.size() + strlen("sumcheck_round_0") + 4 * 32 + strlen("sumcheck_challenge_0"));
+    ScHostRounds H;  // (rounds rh .. nv - 1)
     for (unsigned rnd = 0; rnd < nv; rnd++) {
-      const uint32_t seq_next = queue(rnd + 1);
+      const uint32_t seq_next = rnd + 1 <= rh ? queue(rnd + 1) : 0;  // (rnd + 1 == rh: the hand-over)
       Fr e[4];
-      sc_round_sums(R, seq, e);
+      if (rnd < rh) {
+        sc_round_sums(R, seq, e);
+      } else {
+        if (rnd == rh) {
+          sc_wait(c, seq);
+          H.load((const Fr *)c->sc_htab.p, k, n >> rh, R.perm, terms, n_terms);
+        }
+        H.sums(e);
+      }
 #if TNS_SC_TRACE
       t_seen[rnd] = us();
 #endif
@@ -1112,7 +1246,8 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
       for (int x = 0; x < 4; x++) tr.append_fr(coeffs[x]);
       snprintf(lab, sizeof lab, "sumcheck_challenge_%u", rnd);
       const Fr ch = tr.challenge(lab);
-      publish(rnd, ch);  // (first: the device's next round waits for it)
+      if (rnd < rh) publish(rnd, ch);  // (first: the device's next round waits for it)
+      else H.fold(ch);
 #if TNS_SC_TRACE
       t_pub[rnd] = us();
 #endif
@@ -1126,7 +1261,7 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
         tr.prehash(tr.state.size() + (size_t)n1 + 4 * 32 + (size_t)n2);
       }
     }
-    const ScResult &res = sc_wait(c, seq);
+    const ScResult &res = rh < nv ? *(const ScResult *)c->sc_mapped.p : sc_wait(c, seq);
 #if TNS_SC_TRACE
     t_seen[nv] = us();
     for (unsigned rnd = 0; rnd < nv; rnd++)
@@ -1144,7 +1279,11 @@ static void sumcheck_prove_terms(Ctx *c, Fr *const *tables, int k, unsigned nv, 
     TNS_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_sc_trace), &nullp, sizeof nullp));
 #endif
     Fr vals[MAX_SC_TABLES];
-    for (int m = 0; m < k; m++) vals[R.perm[m]] = res.sums[m];
+    if (rh < nv) {
+      for (int i = 0; i < k; i++) vals[i] = H.t[i][0].fp();
+    } else {
+      for (int m = 0; m < k; m++) vals[R.perm[m]] = res.sums[m];
+    }
     for (int i = 0; i < k; i++) final_vals[i] = vals[i];
     *final_eval = eval_composition_host(vals, terms, n_terms);  // polynomial(&fixed_variables), :104
     // the last round's claim is g_{nv-1}(r_{nv-1}) = f(r): an honest prover's final value must

@@ -757,8 +757,10 @@ static SortInput bits_launch(MsmLane &ln, const Fr *scalars, size_t n) {
   in.fr = scalars;
   in.mont = true;
   const MsmLane::PlanHint &h = ln.hint;
+  // (narrow per-window plans -- the trace values -- also get their canonical low 64 bits written)
+  const bool narrow = !h.shared && h.c * h.W <= 64;
   if (!(h.n == n && h.c > 0 &&
-        bucket_sort_precount_bits(ln, scalars, n, h.c, h.W, h.shared, h.bucket_bits, d_bits, in))) {
+        bucket_sort_precount_bits(ln, scalars, n, h.c, h.W, h.shared, h.bucket_bits, d_bits, in, narrow))) {
     k_scalar_bits<<<grid_for(n, 256, 2048), 256, 0, ln.stream>>>(scalars, n, d_bits, nullptr);
     TNS_LAUNCH_CHECK();
   }
@@ -849,6 +851,13 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   }
   finish_plan(P);
   if (in.mont && in.fr && !in.u64) ln.hint = MsmLane::PlanHint{n, P.c, P.W, P.end_bit - 1, P.shared};
+  SortInput in2 = in;
+  if (in.low64 && bits <= 64) {  // the scalars fit 64 bits: the sort reads their canonical low words
+    in2.u64 = in.low64;
+    in2.n_u64 = n;
+    in2.fr = nullptr;
+    in2.mont = false;
+  }
   const size_t total = (size_t)P.W * n;
   if (total >= ((size_t)1 << 31)) throw Error(TNS_ERR_COMMITMENT, "MSM too large for one sort");
 
@@ -859,7 +868,7 @@ static void msm_launch_sort(Ctx *ctx, MsmLane &ln, const G1Affine *points, const
   J.n = n;
   J.sort_prof.reset(new ProfScope(ctx->prof, st, "msm_sort", 32.0 * n + 16.0 * total));
   J.valid = (uint32_t *)ln.ws[4].ensure(2 * sizeof(uint32_t));  // entries; [1]: a run crosses a chunk
-  bucket_sort_begin(ln, in, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
+  bucket_sort_begin(ln, in2, n, P.c, P.W, P.shared, (uint32_t)P.stride, P.end_bit - 1, J.valid, J.bs);
   J.sort_pending = true;
   J.passes_pending = true;
   if (!defer) msm_finish_sort(J);
