@@ -47,6 +47,7 @@ Ctx::~Ctx() {
   if (lanes[1].stream) (void)hipStreamDestroy(lanes[1].stream);
   if (side) (void)hipStreamDestroy(side);
   if (copy) (void)hipStreamDestroy(copy);
+  if (acc) (void)hipStreamDestroy(acc);
   for (hipEvent_t e : stage_ev)
     if (e) (void)hipEventDestroy(e);
   if (stream) (void)hipStreamDestroy(stream);
@@ -411,13 +412,16 @@ int tns_ctx_create(int device, tns_ctx **out) {
       throw Error(TNS_ERR_NO_DEVICE, std::string("libtns is built for gfx950, device is ") + prop.gcnArchName);
     tns_ctx *x = new tns_ctx();
     x->c.device = device;
-    TNS_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
-    x->c.lanes[0].stream = x->c.stream;
     int prio_lo = 0, prio_hi = 0;
     TNS_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    // three levels: the context stream (lane 0) above lane 1 above an MSM pair's accumulations
+    // (msm_pair_dev): sort and tail blocks dispatch ahead of accumulation blocks where they fit
+    // beside them (a 72 KB-LDS scatter block that does not fit still waits: DESIGN.md section 10)
+    TNS_HIP(hipStreamCreateWithPriority(&x->c.stream, hipStreamNonBlocking, prio_hi));
+    TNS_HIP(hipStreamCreateWithFlags(&x->c.lanes[1].stream, hipStreamNonBlocking));
+    TNS_HIP(hipStreamCreateWithPriority(&x->c.acc, hipStreamNonBlocking, prio_lo));
+    x->c.lanes[0].stream = x->c.stream;
     x->c.num_cu = prop.multiProcessorCount;
-    (void)prio_hi;
-    TNS_HIP(hipStreamCreateWithPriority(&x->c.lanes[1].stream, hipStreamNonBlocking, prio_lo));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
     TNS_HIP(hipStreamCreateWithFlags(&x->c.copy, hipStreamNonBlocking));
     *out = x;
@@ -430,6 +434,7 @@ void tns_ctx_destroy(tns_ctx *ctx) {
   (void)hipSetDevice(ctx->c.device);
   (void)hipStreamSynchronize(ctx->c.stream);
   if (ctx->c.side) (void)hipStreamSynchronize(ctx->c.side);
+  if (ctx->c.acc) (void)hipStreamSynchronize(ctx->c.acc);
   delete ctx;
 }
 

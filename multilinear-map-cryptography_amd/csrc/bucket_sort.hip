@@ -176,14 +176,11 @@ static_assert(BS_MAXBINS <= 2 * BS_BLOCK, "two bins per thread in the block scan
 // opening, their ~64-byte runs of half-dword stores costing more than the bytes saved.)
 enum { KF_U32 = 0, KF_U16 = 1 };
 
-// the scatters' stores (TNS_BS_NT build: non-temporal, A/B)
+// the scatters' stores (plain: non-temporal stores measured +1.3-2.1 ms per C4 step,
+// profiles/r06_ab_sort_nt.txt)
 template <class T>
 __device__ __forceinline__ void st_out(T *p, T v) {
-#if defined(TNS_BS_NT) && TNS_BS_NT
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
 }
 
 __device__ __forceinline__ void store_entry(int kf, uint32_t *__restrict__ okeys, uint32_t *__restrict__ ovals,

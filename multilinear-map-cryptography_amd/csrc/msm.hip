@@ -904,13 +904,13 @@ static void msm_finish_sort(MsmJob &J) {
 
 // Phase 2 (asynchronous): accumulation, bucket fixup, reduction and the per-set sums' readback.
 // `accumulated` (optional) is recorded on the lane right after the accumulation kernel.
-static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated) {
+static void msm_launch_accumulate(Ctx *ctx, MsmJob &J, hipEvent_t accumulated, hipStream_t on = nullptr) {
   if (!J.sorted) {  // immediate / tiny: done in phase 1
-    if (accumulated) TNS_HIP(hipEventRecord(accumulated, J.lane->stream));
+    if (accumulated) TNS_HIP(hipEventRecord(accumulated, on ? on : J.lane->stream));
     return;
   }
   MsmLane &ln = *J.lane;
-  hipStream_t st = ln.stream;
+  hipStream_t st = on ? on : ln.stream;
   if (!J.buckets) J.buckets = (G1Xyzz *)ln.ws[5].ensure(sizeof(G1Xyzz) * J.P.nb);
   HeadTail *ht = (HeadTail *)ln.ws[6].ensure(sizeof(HeadTail) * J.nchunks);
   {
@@ -1182,51 +1182,46 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   msm_sort_passes(ja);
   msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, true);
   msm_sort_passes(jb);
-  msm_finish_sort(ja);
-  msm_finish_sort(jb);
-  // both (memory-bound) sorts first, then both accumulations: an accumulation launched while the
-  // other lane still sorts takes every slot and stalls that sort behind it
-  TNS_HIP(hipStreamWaitEvent(l0.stream, sb, 0));
-  TNS_HIP(hipStreamWaitEvent(l1.stream, sa, 0));
-  (void)hipEventDestroy(sa);
-  (void)hipEventDestroy(sb);
-  // The accumulations run one after the other (each is VALU-bound on the whole chip: run together
-  // they take as long, and each launch's own duration is then its kernel time).  A pair of
-  // table-window MSMs (the openings: full-width scalars, ~17 ms accumulations) then runs both
+  // Both accumulations go on the context's least-priority stream (ctx->acc), one after the other
+  // (each is VALU-bound on the whole chip: run together they take as long), each as soon as its
+  // own sort is done: the first runs beside the rest of lane 1's sort, which then finishes in the
+  // first accumulation's tail-off.  Waiting for both sorts first left the chip to lane 1's last
+  // passes alone for ~1.2 ms; this is 0.4 ms faster per C4 step
+  // (profiles/r06_ab_acc_stream.txt) -- lane 1's sort stage then spans the first accumulation.
+  // A pair of table-window MSMs (the openings: full-width scalars, ~16 ms accumulations) runs both
   // tails after the second accumulation as ONE two-set launch sequence on lane 0 (tails under the
   // second accumulation took wave slots from it, profiles/r02_ab_tails_last.txt); the commitments
   // keep lane 0's tail under lane 1's accumulation (the 22-bit address MSM's 2^22-bucket reduction
   // is longer than the value accumulation).
-  const bool tails_last = ja.sorted && jb.sorted && ja.P.shared && jb.P.shared;
-  hipEvent_t acc_a;
+  hipStream_t as = ctx->acc;
+  msm_finish_sort(ja);
+  hipEvent_t acc_a, acc_b;
   TNS_HIP(hipEventCreateWithFlags(&acc_a, hipEventDisableTiming));
-  if (tails_last) {
-    const bool two_set = same_tail_shape(ja, jb);
-    if (two_set) {  // the pair's buckets adjoin: one reduction over two sets
-      ja.buckets = (G1Xyzz *)l0.ws[5].ensure(sizeof(G1Xyzz) * 2 * ja.P.nb);
-      jb.buckets = ja.buckets + ja.P.nb;
-    }
-    hipEvent_t acc_b;
-    TNS_HIP(hipEventCreateWithFlags(&acc_b, hipEventDisableTiming));
-    msm_launch_accumulate(ctx, ja, acc_a);
-    TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
-    msm_launch_accumulate(ctx, jb, acc_b);
-    TNS_HIP(hipStreamWaitEvent(l0.stream, acc_b, 0));
-    (void)hipEventDestroy(acc_b);
-    if (two_set) {
-      MsmJob *both[2] = {&ja, &jb};
-      msm_launch_tails(ctx, both, 2, l0);
-    } else {
-      MsmJob *one_a[1] = {&ja}, *one_b[1] = {&jb};
-      msm_launch_tails(ctx, one_a, 1, l0);
-      msm_launch_tails(ctx, one_b, 1, l1);
-    }
+  TNS_HIP(hipEventCreateWithFlags(&acc_b, hipEventDisableTiming));
+  // a two-set tail needs the pair's buckets adjoining: room for both before acc a writes the first
+  if (ja.sorted && ja.P.shared) ja.buckets = (G1Xyzz *)l0.ws[5].ensure(sizeof(G1Xyzz) * 2 * ja.P.nb);
+  TNS_HIP(hipStreamWaitEvent(as, sa, 0));
+  msm_launch_accumulate(ctx, ja, acc_a, as);
+  msm_finish_sort(jb);
+  const bool tails_last = ja.sorted && jb.sorted && ja.P.shared && jb.P.shared;
+  const bool two_set = tails_last && same_tail_shape(ja, jb);
+  if (two_set) jb.buckets = ja.buckets + ja.P.nb;
+  TNS_HIP(hipStreamWaitEvent(as, sb, 0));
+  msm_launch_accumulate(ctx, jb, acc_b, as);
+  (void)hipEventDestroy(sa);
+  (void)hipEventDestroy(sb);
+  TNS_HIP(hipStreamWaitEvent(l0.stream, tails_last ? acc_b : acc_a, 0));
+  if (two_set) {
+    MsmJob *both[2] = {&ja, &jb};
+    msm_launch_tails(ctx, both, 2, l0);
   } else {
-    msm_launch_reduce(ctx, ja, acc_a);
-    TNS_HIP(hipStreamWaitEvent(l1.stream, acc_a, 0));
-    msm_launch_reduce(ctx, jb);
+    TNS_HIP(hipStreamWaitEvent(l1.stream, acc_b, 0));
+    MsmJob *one_a[1] = {&ja}, *one_b[1] = {&jb};
+    msm_launch_tails(ctx, one_a, 1, l0);
+    msm_launch_tails(ctx, one_b, 1, l1);
   }
   (void)hipEventDestroy(acc_a);
+  (void)hipEventDestroy(acc_b);
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
 }
