@@ -266,9 +266,15 @@ static void commit_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1
 
 // extra (optional): exchanged with the openings' partial sums once extra_ready() has run (the
 // sharded sum-check's folded table values, which the side stream computes under the openings)
+// side_work (optional): host work to queue once the barycentric pass is on the device (it runs
+// before the pass's first host wait instead of in front of its launches)
 static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, const Fr &z, Fr value[2],
                             G1Affine proof[2], DevBuf &sbuf0, DevBuf &sbuf1, Comm &m,
-                            ExtraPayload *extra = nullptr, const std::function<void()> &extra_ready = nullptr) {
+                            ExtraPayload *extra = nullptr, const std::function<void()> &extra_ready = nullptr,
+                            const std::function<void()> &side_work = nullptr) {
+  const bool same_nodes = p0.N == p1.N && p0.first == p1.first && p0.cnt == p1.cnt;
+  const bool pair_pass = p0.basis && p1.basis && !fr_is_node(z, p0.N) && !fr_is_node(z, p1.N) && same_nodes;
+  if (side_work && !pair_pass) side_work();
   if (!p0.basis || !p1.basis || fr_is_node(z, p0.N) || fr_is_node(z, p1.N)) {
     open_evals(c, srs, p0, z, &value[0], &proof[0], sbuf0, m);
     open_evals(c, srs, p1, z, &value[1], &proof[1], sbuf0, m);
@@ -280,14 +286,13 @@ static void open_evals_pair(Ctx *c, const Srs &srs, EvalPoly &p0, EvalPoly &p1, 
   }
   Fr *q0 = (Fr *)sbuf0.ensure(sizeof(Fr) * p0.cnt), *q1 = (Fr *)sbuf1.ensure(sizeof(Fr) * p1.cnt);
   Fr part[4];
-  const bool same_nodes = p0.N == p1.N && p0.first == p1.first && p0.cnt == p1.cnt;
   // the shared-inverse pass hands the MSMs canonical quotients and their bit lengths; its
   // inverses come out canonical too, so the quotient kernel needs no reduction pass
   // (0.540 -> 0.504 ms at C4, profiles/r04_c4_step_timeline_canon_inv.txt)
   const bool canon_q = same_nodes && p0.cnt > 64, canon_inv = canon_q;
   if (same_nodes) {  // Twist: one batch inversion for both vectors (inverses land in q1)
     Fr p3[3];
-    lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3, canon_inv);
+    lagrange_open_partial2_dev(c, p0.y, p1.y, p0.N, p0.first, p0.cnt, z, q1, p3, canon_inv, side_work);
     part[0] = part[2] = p3[0];
     part[1] = p3[1];
     part[3] = p3[2];
@@ -961,6 +966,8 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   // values are collected at the end of the proof
   // (queued behind the quotient kernel instead, under the opening sorts: a tie, 49.19-49.51 vs
   // 49.32-49.51 ms per step, profiles/r04_ab_folds_at.txt)
+  // (queued once the openings' barycentric pass is on the device: its launches come first, and the
+  // folds' ~80 us of host launches run under its chain kernels, profiles/r06_hiptrace_gaps.txt)
   Fr *d_vals = (Fr *)c->sc_out.ensure(sizeof(Fr) * 4);
   {
     hipEvent_t ready;
@@ -968,9 +975,14 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     TNS_HIP(hipEventRecord(ready, c->stream));  // the tables were written on the context stream
     TNS_HIP(hipStreamWaitEvent(c->side, ready, 0));
     (void)hipEventDestroy(ready);
+  }
+  bool folds_queued = false;
+  auto queue_folds = [&]() {
+    if (folds_queued) return;
+    folds_queued = true;
     sumcheck_zero_folds_async(c, c->side, mles, n_mles, nv_loc, chal, d_vals, flags, n_flags);
     TNS_HIP(hipMemcpyAsync(vals, d_vals, sizeof(Fr) * n_mles, hipMemcpyDeviceToHost, c->side));
-  }
+  };
   const Fr fe = Fr::zero();
   out->num_rounds = nv;
   std::memcpy(out->round_polynomials, rounds.data(), 128 * (size_t)nv);
@@ -989,6 +1001,7 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
   fold_x.bytes = sizeof(Fr) * (size_t)n_mles;
   bool folds_exchanged = false;
   auto folds_ready = [&]() {
+    queue_folds();
     TNS_HIP(hipStreamSynchronize(c->side));
     for (int j = 0; j < n_mles; j++) finals[j] = vals[j];
   };
@@ -997,7 +1010,8 @@ static void fill_common_tail(Ctx *c, const Srs &srs, HostTranscript &tr, Fr *con
     std::memcpy(out->opening_point, &z, 32);
     Fr v[2];
     G1Affine pi[2];
-    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m, lr ? &fold_x : nullptr, folds_ready);
+    open_evals_pair(c, srs, polyA, polyB, z, v, pi, sbuf, c->prove_ws[10], m, lr ? &fold_x : nullptr, folds_ready,
+                    queue_folds);
     folds_exchanged = lr > 0;
     store_proj(pi[0], out->opening_proofs[0]);
     store_proj(pi[1], out->opening_proofs[1]);

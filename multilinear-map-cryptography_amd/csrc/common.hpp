@@ -636,8 +636,11 @@ void lagrange_open_partial_dev(Ctx *c, const Fr *y, size_t N, size_t first, size
 // q_i = (v - y_i) * inv_i in place: the quotient's values on the slice
 void lagrange_quotient_finish_dev(Ctx *c, const Fr *y, size_t cnt, const Fr &v, Fr *q);
 // canon_inv: inv receives the inverses in canonical form (for the CI quotient kernel)
+// queued (optional): run on the host once the pass's first kernels are queued, before its first
+// host wait (side-stream work that should not delay the pass)
 void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
-                                Fr *inv, Fr parts[3], bool canon_inv = false);
+                                Fr *inv, Fr parts[3], bool canon_inv = false,
+                                const std::function<void()> &queued = nullptr);
 // bits != nullptr: q0 / q1 come out CANONICAL with their largest bit lengths in bits[0..1];
 // canon_inv (requires bits): inv holds canonical inverses (lagrange_open_partial2_dev's canon_inv)
 void lagrange_quotient_finish2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t cnt, const Fr &v0, const Fr &v1,

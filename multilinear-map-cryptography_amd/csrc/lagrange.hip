@@ -418,7 +418,7 @@ struct NodeSweep {
 
 // chains over the local nodes i < n of x' = x - first (so x' - i = x - j); dev[0] = prod
 static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_t skip = SIZE_MAX,
-                                   const Fr &scale = Fr::one()) {
+                                   const Fr &scale = Fr::one(), const std::function<void()> &queued = nullptr) {
   NodeSweep s;
   s.T = chain_count(n);
   s.Tm = from_u64<FrCfg>((uint64_t)s.T);
@@ -437,6 +437,7 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   if (nb > 1024) {  // (more than 2^18 chains: one inverse per block, on the device)
     k_chain_inv<<<nb, 256, 0, c->stream>>>(s.cp, s.T, s.icp, scale);
     TNS_LAUNCH_CHECK();
+    if (queued) queued();
     return s;
   }
   k_chain_local<<<nb, 256, 0, c->stream>>>(s.cp, s.T, s.icp, tot);
@@ -446,6 +447,7 @@ static NodeSweep node_sweep_begin(Ctx *c, const Fr &xs, size_t n, Fr *pre, size_
   k_chain_totals<<<1, 256, 0, c->stream>>>(tot, (int)nb, oth, (Fr *)((char *)c->inv_mapped.dev + 64),
                                            (uint32_t *)c->inv_mapped.dev, seq);
   TNS_LAUNCH_CHECK();
+  if (queued) queued();  // (under the chain kernels, ~0.6 ms at C4)
   const volatile uint32_t *flag = (const volatile uint32_t *)m;
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned spin = 1; __atomic_load_n((const uint32_t *)flag, __ATOMIC_ACQUIRE) != seq; spin++)
@@ -558,7 +560,7 @@ void lagrange_node_quotient_dev(Ctx *c, const Fr *y, size_t N, size_t j0, Fr *q)
 // the products along the chain keep the factor), for lagrange_quotient_finish2_dev's CI form;
 // the sums then carry it too and are scaled back by R (the raw R^2) after the readback.
 void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, size_t first, size_t cnt, const Fr &z,
-                                Fr *inv, Fr parts[3], bool canon_inv) {
+                                Fr *inv, Fr parts[3], bool canon_inv, const std::function<void()> &queued) {
   TNS_PROF(c, "open_scan", 32.0 * 5 * cnt);  // pre write/read, inv write, y0, y1, w
   const Fr *w = bary_weights(c, N, first, cnt);
   const Fr xs = fr_shift(z, first);
@@ -567,7 +569,7 @@ void lagrange_open_partial2_dev(Ctx *c, const Fr *y0, const Fr *y1, size_t N, si
     scale = Fr::zero();
     scale.v[0] = 1;
   }
-  NodeSweep s = node_sweep_begin(c, xs, cnt, inv, SIZE_MAX, scale);
+  NodeSweep s = node_sweep_begin(c, xs, cnt, inv, SIZE_MAX, scale, queued);
   k_node_finish2<<<grid_for(s.T, 256, 1u << 30), 256, 0, c->stream>>>(xs, cnt, s.T, s.Tm, inv, s.icp, s.inverted, scale,
                                                                       w, y0, y1, inv, s.sp);
   TNS_LAUNCH_CHECK();

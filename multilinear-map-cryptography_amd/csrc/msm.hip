@@ -727,6 +727,12 @@ void lane_publish_slot(MsmLane &ln, int slot, uint32_t **data, uint32_t **flag, 
   *flag = (uint32_t *)(dev + 64 * slot);
 }
 
+// the slot's publish has landed (no wait)
+static bool lane_ready(MsmLane &ln, int slot) {
+  const uint32_t *flag = (const uint32_t *)((const char *)ln.mapped.p + 64 * slot);
+  return __atomic_load_n(flag, __ATOMIC_ACQUIRE) == ln.slot_seq[slot];
+}
+
 const void *lane_wait(MsmLane &ln, int slot) {
   const char *m = (const char *)ln.mapped.p;
   const uint32_t *flag = (const uint32_t *)(m + 64 * slot), seq = ln.slot_seq[slot];
@@ -1222,6 +1228,20 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   }
   (void)hipEventDestroy(acc_a);
   (void)hipEventDestroy(acc_b);
+  // two tails on two lanes: the host's part (bucket-sum Horner, ~20-45 us) of whichever lands
+  // first runs while the other lane's tail still runs on the device
+  if (!two_set && jb.res_lane && jb.res_lane != ja.res_lane && jb.sorted && ja.sorted) {
+    // (bounded: past it the plain order below, whose waits report a faulted stream)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spin = 1; !lane_ready(*ja.res_lane, LANE_SLOT_SUMS) && !lane_ready(*jb.res_lane, LANE_SLOT_SUMS);
+         spin++)
+      if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) break;
+    if (!lane_ready(*ja.res_lane, LANE_SLOT_SUMS) && lane_ready(*jb.res_lane, LANE_SLOT_SUMS)) {
+      out[1] = msm_complete(ctx, jb);
+      out[0] = msm_complete(ctx, ja);
+      return;
+    }
+  }
   out[0] = msm_complete(ctx, ja);
   out[1] = msm_complete(ctx, jb);
 }
