@@ -620,7 +620,8 @@ def main():
     world, rank, local, pg = dist_setup(args)
     import twist_and_shout as ts
 
-    ctx = ts.Context.get(local)
+    # (several processes on one GPU: no least-priority queue to starve behind the others')
+    ctx = ts.Context.get(local, stream_priorities=not args.rehearse_one_gpu)
     sharded = world > 1 and not args.independent
     comm_cfg = None
     # operations of ONE proof: C4 (2^24) at N = 1, C5 (2^26, setup_params(24)) at N > 1

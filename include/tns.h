@@ -109,6 +109,15 @@ int tns_device_info_get(int device, tns_device_info *out);
 
 /* ---------------------------------------------------------------- context */
 int tns_ctx_create(int device, tns_ctx **out);
+/* tns_ctx_create with flags (0 = tns_ctx_create).  By default an MSM pair's accumulations run on
+ * a least-priority stream and the context stream at the greatest priority, which orders the pair's
+ * second sort behind the first accumulation (C4: -0.3-0.45 ms a proof).
+ * TNS_CTX_NO_STREAM_PRIORITIES: every stream at the default priority -- for processes that share
+ * one GPU, whose least-priority queues otherwise starve behind the other processes' (4 processes
+ * on one GPU: 190 -> 330-360 ms a proof).  Same proofs either way; unknown flags ->
+ * TNS_ERR_INVALID_PARAMETERS. */
+#define TNS_CTX_NO_STREAM_PRIORITIES 1u
+int tns_ctx_create_ex(int device, unsigned flags, tns_ctx **out);
 void tns_ctx_destroy(tns_ctx *ctx);
 int tns_ctx_synchronize(tns_ctx *ctx);
 
@@ -169,7 +178,8 @@ int tns_ctx_set_msm_tables(tns_ctx *ctx, int on);
  * equal node ranges (1..64, default 4), each committed by its own MSM as soon as it lands, so only
  * the last range's MSM follows the link (C4: commit phase 19.0 -> 15.5 ms at 4).  Same proofs
  * for every setting; out of range -> TNS_ERR_INVALID_PARAMETERS.  The library reads no tuning
- * from the environment: this and the two setters above are its whole tuning surface. */
+ * from the environment: this, the two setters above and tns_ctx_create_ex's flags are its
+ * whole tuning surface. */
 int tns_ctx_set_upload_chunks(tns_ctx *ctx, int chunks);
 
 /* ---------------------------------------------------------------- KZG (src/commitments.rs) */

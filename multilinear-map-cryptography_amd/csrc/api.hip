@@ -404,8 +404,36 @@ int tns_device_info_get(int device, tns_device_info *out) {
   });
 }
 
-int tns_ctx_create(int device, tns_ctx **out) {
+// The context's five streams.  Created in this order: with GPU_MAX_HW_QUEUES = 4 (HIP's default)
+// the fifth stream shares the first one's hardware queue, and the copy stream (drop-in uploads,
+// during the commitments) and the accumulation stream (only in the openings of a drop-in proof)
+// are never busy together -- the copy stream on the context stream's queue serialised the upload
+// behind the commitments (+1.4 ms per drop-in C4 step, profiles/r06_ab_stream_priority.txt).
+// prio: the accumulations at the least priority and the context stream (lane 0) at the greatest,
+// lane 1 / side / copy normal -- lane 1's last sort passes then wait for the first accumulation's
+// tail-off instead of running beside it (-0.3-0.45 ms per C4 step); off for processes sharing a
+// GPU, whose least-priority queues starve behind the other processes' (TNS_CTX_NO_STREAM_PRIORITIES;
+// chosen at creation: streams recreated without priorities in the same process kept the pathology).
+static void create_streams(Ctx &c, bool prio) {
+  int lo = 0, hi = 0;
+  TNS_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  if (!prio) lo = hi = 0;
+  auto mk = [](hipStream_t *s, int p) {
+    TNS_HIP(p ? hipStreamCreateWithPriority(s, hipStreamNonBlocking, p) : hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  };
+  mk(&c.acc, lo);
+  mk(&c.stream, hi);
+  c.lanes[0].stream = c.stream;
+  mk(&c.lanes[1].stream, 0);
+  mk(&c.side, 0);
+  mk(&c.copy, 0);
+}
+
+int tns_ctx_create(int device, tns_ctx **out) { return tns_ctx_create_ex(device, 0, out); }
+
+int tns_ctx_create_ex(int device, unsigned flags, tns_ctx **out) {
   return guarded([&]() {
+    if (flags & ~TNS_CTX_NO_STREAM_PRIORITIES) throw Error(TNS_ERR_INVALID_PARAMETERS, "unknown context flags");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
       throw Error(TNS_ERR_NO_DEVICE, "no HIP device visible");
@@ -417,18 +445,13 @@ int tns_ctx_create(int device, tns_ctx **out) {
       throw Error(TNS_ERR_NO_DEVICE, std::string("libtns is built for gfx950, device is ") + prop.gcnArchName);
     tns_ctx *x = new tns_ctx();
     x->c.device = device;
-    int prio_lo = 0, prio_hi = 0;
-    TNS_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    // three levels: the context stream (lane 0) above lane 1 above an MSM pair's accumulations
-    // (msm_pair_dev): sort and tail blocks dispatch ahead of accumulation blocks where they fit
-    // beside them (a 72 KB-LDS scatter block that does not fit still waits: DESIGN.md section 10)
-    TNS_HIP(hipStreamCreateWithPriority(&x->c.stream, hipStreamNonBlocking, prio_hi));
-    TNS_HIP(hipStreamCreateWithFlags(&x->c.lanes[1].stream, hipStreamNonBlocking));
-    TNS_HIP(hipStreamCreateWithPriority(&x->c.acc, hipStreamNonBlocking, prio_lo));
-    x->c.lanes[0].stream = x->c.stream;
     x->c.num_cu = prop.multiProcessorCount;
-    TNS_HIP(hipStreamCreateWithFlags(&x->c.side, hipStreamNonBlocking));
-    TNS_HIP(hipStreamCreateWithFlags(&x->c.copy, hipStreamNonBlocking));
+    try {
+      create_streams(x->c, !(flags & TNS_CTX_NO_STREAM_PRIORITIES));
+    } catch (...) {
+      delete x;
+      throw;
+    }
     *out = x;
     return TNS_OK;
   });

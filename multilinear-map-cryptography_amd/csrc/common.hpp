@@ -308,9 +308,9 @@ struct Ctx {
   DevBuf sc_tail_sync;                  // ... and relayed between the blocks of the persistent tail
   uint32_t sc_chal_seq = 0;             // the flag value of the latest published challenge
   PinnedBuf sc_host;    // its challenges (in) and bound table values (out)
-  hipStream_t side = nullptr;  // work no later launch waits for (the zero-closure folds)
+  hipStream_t side = nullptr;  // the zero-closure folds
   hipStream_t copy = nullptr;  // host-buffer uploads that overlap a proof's first MSM (HostUpload)
-  hipStream_t acc = nullptr;   // an MSM pair's accumulations (least priority: msm_pair_dev)
+  hipStream_t acc = nullptr;   // an MSM pair's accumulations (msm_pair_dev)
   PinnedBuf stage;             // their pinned staging ring (upload.cpp, built on first use)
   hipEvent_t stage_ev[32] = {};  // upload.cpp's staging ring: one event per slot
   DevBuf qbits;        // opening quotients' bit lengths (lagrange_quotient_finish2_dev)

@@ -1188,11 +1188,11 @@ void msm_pair_dev(Ctx *ctx, const MsmArgs &a, const MsmArgs &b, G1Xyzz out[2]) {
   msm_sort_passes(ja);
   msm_launch_sort(ctx, l1, b.points, b.scalars, cb, b.n, b.fb, bb, jb, sb, true);
   msm_sort_passes(jb);
-  // Both accumulations go on the context's least-priority stream (ctx->acc), one after the other
-  // (each is VALU-bound on the whole chip: run together they take as long), each as soon as its
-  // own sort is done: the first runs beside the rest of lane 1's sort, which then finishes in the
-  // first accumulation's tail-off.  Waiting for both sorts first left the chip to lane 1's last
-  // passes alone for ~1.2 ms; this is 0.4 ms faster per C4 step
+  // Both accumulations go on the context's side stream (free here: its folds run before the
+  // openings' MSMs), one after the other (each is VALU-bound on the whole chip: run together they
+  // take as long), each as soon as its own sort is done: the first runs beside the rest of lane 1's
+  // sort, which then finishes in the first accumulation's tail-off.  Waiting for both sorts first
+  // left the chip to lane 1's last passes alone for ~1.2 ms; this is 0.4 ms faster per C4 step
   // (profiles/r06_ab_acc_stream.txt) -- lane 1's sort stage then spans the first accumulation.
   // A pair of table-window MSMs (the openings: full-width scalars, ~16 ms accumulations) runs both
   // tails after the second accumulation as ONE two-set launch sequence on lane 0 (tails under the

@@ -139,18 +139,22 @@ class Context:
     _lock = threading.Lock()
     _by_device: dict = {}
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, stream_priorities: bool = True):
+        """stream_priorities=False (TNS_CTX_NO_STREAM_PRIORITIES): every stream at the default
+        priority, for processes that share one GPU.  Same proofs."""
         lib = N.load()
         h = C.c_void_p()
-        _check(lib.tns_ctx_create(device, C.byref(h)))
+        _check(lib.tns_ctx_create_ex(device, 0 if stream_priorities else 1, C.byref(h)))
         self.handle = h
         self.device = device
+        self.stream_priorities = stream_priorities
 
     @classmethod
-    def get(cls, device: int = 0) -> "Context":
+    def get(cls, device: int = 0, stream_priorities: bool = True) -> "Context":
+        """The process's context on `device` (the first call creates it with `stream_priorities`)."""
         with cls._lock:
             if device not in cls._by_device:
-                cls._by_device[device] = Context(device)
+                cls._by_device[device] = Context(device, stream_priorities)
             return cls._by_device[device]
 
     def __del__(self):

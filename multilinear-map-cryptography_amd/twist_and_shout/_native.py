@@ -79,6 +79,7 @@ SIGNATURES = [
     ("tns_device_count", C.c_int, []),
     ("tns_device_info_get", C.c_int, [C.c_int, C.POINTER(TnsDeviceInfo)]),
     ("tns_ctx_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("tns_ctx_create_ex", C.c_int, [C.c_int, C.c_uint, C.POINTER(C.c_void_p)]),
     ("tns_ctx_destroy", None, [C.c_void_p]),
     ("tns_ctx_synchronize", C.c_int, [C.c_void_p]),
     ("tns_setup_params", C.c_int, [C.c_void_p, C.c_uint, C.POINTER(TnsParams), C.POINTER(C.c_void_p)]),

@@ -41,8 +41,20 @@ def test_version_and_no_silent_fallback():
         h = C.c_void_p()
         st = lib.tns_ctx_create(0, C.byref(h))
         assert st == 101, N.last_error()
+        st = lib.tns_ctx_create_ex(0, 1, C.byref(h))  # TNS_CTX_NO_STREAM_PRIORITIES
+        assert st == 101, N.last_error()
+        with pytest.raises(ts.TwistAndShoutError):
+            ts.Context(0, stream_priorities=False)
         with pytest.raises(ts.TwistAndShoutError):
             ts.Context(0)
+
+
+def test_ctx_create_ex_unknown_flags():
+    """Unknown context flags are refused before anything touches a device."""
+    lib = N.load()
+    h = C.c_void_p()
+    assert lib.tns_ctx_create_ex(0, 2, C.byref(h)) == 1, N.last_error()  # TNS_ERR_INVALID_PARAMETERS
+    assert "flags" in N.last_error()
 
 
 def test_c_host_refuses_without_device():

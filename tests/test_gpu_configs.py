@@ -188,3 +188,25 @@ def test_upload_chunks_out_of_range():
     for bad in (0, -1, 65):
         with pytest.raises(ts.InvalidParameters):
             ctx.set_upload_chunks(bad)
+
+
+def test_context_without_stream_priorities_same_proofs():
+    """tns_ctx_create_ex(TNS_CTX_NO_STREAM_PRIORITIES) (processes sharing a GPU): a private context
+    with every stream at the default priority gives the same resident and drop-in Twist proofs and
+    Shout proofs as the default context (the pair accumulations' stream priority only changes the
+    order blocks dispatch in)."""
+    L = 14
+    pp, _ = params(L)
+    n = 1 << (L + 2)
+    addr, val, isw = ts.bench_trace(1 << L, n)
+    entries = ts.to_mont([i * i for i in range(1 << 10)])
+    idx = (np.arange(1 << 12, dtype=np.uint64) * 7) % (1 << 10)
+    want = ts.Twist(pp).prove_soa(addr, val, isw)
+    want_s = ts.Shout(pp).prove_arrays(entries, idx)
+    ctx = ts.Context(0, stream_priorities=False)
+    assert not ctx.stream_priorities
+    pq, _ = ts.setup_params_shard(L, 0, 1, ctx=ctx)
+    d = [ts.DeviceBuffer(ctx, x) for x in (addr, val, isw)]
+    assert ts.twist_proof_from_raw(ts.twist_prove_resident(pq, *d, n)) == want
+    assert ts.Twist(pq).prove_soa(addr, val, isw) == want
+    assert ts.Shout(pq).prove_arrays(entries, idx) == want_s
