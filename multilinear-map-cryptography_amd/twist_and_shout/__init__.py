@@ -404,15 +404,19 @@ def setup_params(log_size: int, device: int = 0) -> Tuple[ProverParams, Verifier
 
 
 # ----------------------------------------------------------------------------- transcript
+_TERMS_CACHE: dict = {}  # SumCheck._terms: composition -> its C array (read-only for the library)
+
+
 class Transcript:
     """src/utils.rs:134-204 (host side; the same code drives the device prover)."""
 
     def __init__(self, seed: bytes = bytes(32)):
-        self._h = N.load().tns_transcript_new((C.c_uint8 * 32)(*seed))
+        self._lib = N.load()
+        self._h = self._lib.tns_transcript_new((C.c_uint8 * 32).from_buffer_copy(bytes(seed)))
 
     def __del__(self):
         try:
-            N.load().tns_transcript_free(self._h)
+            self._lib.tns_transcript_free(self._h)
         except Exception:
             pass
 
@@ -763,10 +767,16 @@ class SumCheck:
 
     @staticmethod
     def _terms(terms):
-        tt = (N.TnsTerm * max(1, len(terms)))()
-        for i, (coef, idx) in enumerate(terms):
-            tt[i].coeff = (C.c_uint64 * 4)(*[int(x) for x in to_mont([coef])[0]])
-            tt[i].tables = (C.c_int32 * 3)(*(list(idx) + [-1] * (3 - len(idx))))
+        # (a composition's C array is built once: the conversions cost ~30 us a call)
+        key = tuple((int(coef), tuple(int(j) for j in idx)) for coef, idx in terms)
+        tt = _TERMS_CACHE.get(key)
+        if tt is None:
+            tt = (N.TnsTerm * max(1, len(terms)))()
+            for i, (coef, idx) in enumerate(key):
+                tt[i].coeff = (C.c_uint64 * 4)(*[int(x) for x in to_mont([coef])[0]])
+                tt[i].tables = (C.c_int32 * 3)(*(list(idx) + [-1] * (3 - len(idx))))
+            if len(_TERMS_CACHE) < 64:
+                _TERMS_CACHE[key] = tt
         return tt
 
     @staticmethod
