@@ -17,7 +17,7 @@ tail -c 300 $out/bench_driverargs.jsonl; echo
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/ks -o run --output-format csv -- python3 bench.py --no-extras --steps 5 --warmup 2 > $out/bench_prof.jsonl 2> $out/bench_prof.err || { tail -20 $out/bench_prof.err; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $out/fetch -o run --output-format csv -- python3 bench.py --no-extras --steps 2 --warmup 1 > $out/fetch.log 2>&1 || exit 1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $out/write -o run --output-format csv -- python3 bench.py --no-extras --steps 2 --warmup 1 > $out/write.log 2>&1 || exit 1
-python3 tools/pmc_summary.py $out 3 > $out/pmc_traffic.json 2> $out/pmc_summary.err || { cat $out/pmc_summary.err; exit 1; }
+python3 tools/pmc_summary.py $out 5 > $out/pmc_traffic.json 2> $out/pmc_summary.err || { cat $out/pmc_summary.err; exit 1; }
 timeout -k 10 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29551 bench.py --gpus 2 --steps 3 --warmup 1 --rehearse-one-gpu > $out/rehearse2.jsonl 2> $out/rehearse2.err || { tail -20 $out/rehearse2.err; exit 1; }
 timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
