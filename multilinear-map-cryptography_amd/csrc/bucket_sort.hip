@@ -731,9 +731,14 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan_apply(const uint32_t *__r
 }
 
 // up to SCAN_SMALL counts in ONE launch: one block of ONE_BLOCK threads walks the array in rounds of
-// ONE_BLOCK x 16 (the segment-count scans of the later passes: 257 .. 65 537 entries, where three
-// launches of a few microseconds each were most of the cost)
-constexpr size_t SCAN_SMALL = (size_t)1 << 17;
+// ONE_BLOCK x 16 (the segment-count scans of the later passes, where three launches of a few
+// microseconds each were most of the cost).  2^15: the last pass of a 2^24-scalar opening MSM has
+// 65 537 segments, whose one-block geometry took ~0.3 ms beside the other lane's scatter (16 serial
+// rounds); the multi-block tiles + scans take ~0.1 ms (C4 -0.17 ms, profiles/r06_ab_sort_geom_threshold.txt)
+#ifndef TNS_SCAN_SMALL_LOG  // (build-time A/B only)
+#define TNS_SCAN_SMALL_LOG 15
+#endif
+constexpr size_t SCAN_SMALL = (size_t)1 << TNS_SCAN_SMALL_LOG;
 __global__ void __launch_bounds__(ONE_BLOCK) k_scan_single(const uint32_t *__restrict__ in, size_t n,
                                                       uint32_t *__restrict__ out) {
   __shared__ uint32_t lds[ONE_BLOCK / 64];
