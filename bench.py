@@ -448,11 +448,14 @@ def sumcheck_generic(ts, ctx, logs):
         sc.prove_resident(tabs, terms, ts.Transcript(bytes(32)), raw=True)  # warm-up
         reps = 5
         # end to end with no profiling (HIP events around every round kernel cost ~10 us a round),
-        # then the round kernels' own time on separate proofs
-        t0 = time.perf_counter()
-        for _ in range(reps):
+        # 20 proofs (mean and median per proof), then the round kernels' own time on separate proofs
+        per = []
+        for _ in range(20):
+            t0 = time.perf_counter()
             sc.prove_resident(tabs, terms, ts.Transcript(bytes(32)), raw=True)
-        dt = (time.perf_counter() - t0) / reps
+            per.append(time.perf_counter() - t0)
+        dt = sum(per) / len(per)
+        dt_med = float(np.median(per))
         ts.profile_enable(ctx, True)
         ts.profile_only(ctx, "sumcheck_round")
         for _ in range(reps):
@@ -465,7 +468,8 @@ def sumcheck_generic(ts, ctx, logs):
         # every round's algorithmic bytes (round 0 reads 64 B per pair and table, later rounds 192 B)
         # over the whole proof's wall time: the persistent tail's rounds carry no HIP events
         all_bytes = sum((64.0 if rr == 0 else 192.0) * (n >> (rr + 1)) * 3 for rr in range(k))
-        out[f"2^{k}"] = {"ms": round(dt * 1e3, 3), "tables": 3, "degree": 3, "rounds": k,
+        out[f"2^{k}"] = {"ms": round(dt * 1e3, 3), "ms_median": round(dt_med * 1e3, 3), "proofs_timed": len(per),
+                         "tables": 3, "degree": 3, "rounds": k,
                          "entries_per_sec": round(3 * n / dt, 1),
                          "kernel_ms": round(kms, 3), "kernel_launches": ex["launches"] // reps,
                          "alg_bytes": ex["bytes"] / reps,

@@ -1,6 +1,7 @@
 """Where a generic sum-check proof's time goes (2^k tables, the bench's Twist-shaped composition):
 wall per call through the Python mirror vs the bare C call, and -- under rocprofv3 --kernel-trace --
-the kernels of the last proof.   python3 tools/sc_trace.py [k] [reps]"""
+the kernels of the last proof.   python3 tools/sc_trace.py [k] [reps] [noprio]
+(noprio: a private context created without stream priorities)"""
 import ctypes as C
 import os
 import sys
@@ -18,7 +19,7 @@ k = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 R = ts.R_MOD
 terms = [(1, [0, 1]), (R - 1, [2, 2, 1]), (2, [2])]
-ctx = ts.Context.get(0)
+ctx = ts.Context(0, stream_priorities=False) if "noprio" in sys.argv[3:] else ts.Context.get(0)
 rng = np.random.default_rng(9)
 n = 1 << k
 tabs = []
