@@ -23,6 +23,9 @@ COMPOSITIONS = {
     "cube4": [(5, [1, 1, 1]), (9, [3]), (1, [0, 2, 3])],
     # four tables, general coefficients at every depth (the K = 4 round kernel's most products)
     "dense4": [(17, [0, 1, 2]), (R - 3, [3, 3]), (5, [1, 2, 3]), (R - 1, [0]), (2, [2, 3]), (7, [])],
+    # one and two tables (the K = 1 / 2 kernels and the host rounds' smallest table sets)
+    "single": [(3, [0, 0, 0]), (R - 2, [0]), (5, [])],
+    "pair2": [(1, [0, 1]), (4, [1, 1])],
 }
 
 
@@ -91,6 +94,20 @@ def test_generic_sumcheck_wrong_claim_at_scale():
 @pytest.mark.parametrize("name", ["twist_like", "dense4"])
 @pytest.mark.parametrize("nv", [0, 1, 2, 3, 4, 5, 13, 14, 15, 16])
 def test_generic_sumcheck_schedule_regimes(name, nv):
+    _regime(name, nv)
+
+
+@pytest.mark.parametrize("name", ["single", "pair2", "mixed", "cube4"])
+@pytest.mark.parametrize("nv", [3, 7, 9, 12])
+def test_generic_sumcheck_host_rounds(name, nv):
+    """The last rounds on the host (from the first round of <= 64 pairs, mle.hip SC_HOST_PAIRS)
+    for one to four tables: at nv = 3 / 7 / 9 the device runs rounds 0-1 and the persistent tail's
+    first round is the hand-over; at nv = 12 the tail runs rounds 2-4 first (512 .. 128 pairs) and
+    the host takes rounds 5-11."""
+    _regime(name, nv)
+
+
+def _regime(name, nv):
     """Every regime of the round schedule against the fold oracle: nv = 0 (the final kernel reads
     the caller's tables as they are), nv = 1 (round 0 then the final fold of the caller's
     tables), 2..5 (the persistent tail from round 2 on), 13..16 (split four-lanes-a-pair rounds up
