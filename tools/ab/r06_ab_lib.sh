@@ -13,6 +13,6 @@ for rep in $(seq 1 $reps); do
     TNS_LIB=$lib timeout -k 10 200 python3 -u bench.py --no-extras --steps 20 --warmup 5 > $out/c4_${v}_$rep.jsonl 2> $out/c4_${v}_$rep.err || { tail -5 $out/c4_${v}_$rep.err; exit 1; }
     echo "$v rep $rep: $(python3 -c "
 import json; d=json.loads(open('$out/c4_${v}_$rep.jsonl').read().strip().splitlines()[-1]); s=d['stages_ms_per_step']
-print('step', d['ms_per_step'], 'acc', d['roofline']['avg_launch_ms'], 'sort', s.get('msm_sort'), 'fixup', s.get('msm_fixup'), 'reduce', s.get('msm_reduce'), 'open_scan', s.get('open_scan'))")" | tee -a $out/summary.txt
+print('step', d['ms_per_step'], 'commit', d['twist_last_prove_ms']['commit'], 'acc', d['roofline']['avg_launch_ms'], 'sort', s.get('msm_sort'), 'fixup', s.get('msm_fixup'), 'reduce', s.get('msm_reduce'), 'open_scan', s.get('open_scan'))")" | tee -a $out/summary.txt
   done
 done
