@@ -136,6 +136,8 @@ __device__ __forceinline__ uint32_t bucket_of(const uint32_t *__restrict__ bstar
   return (uint32_t)lo;
 }
 
+constexpr int FIX_FAN = 8;  // short peel chains: single-thread add chains are latency-bound
+
 // keys == nullptr (values-only sort tail): a chunk finds its first bucket by a binary search of the
 // bucket starts and every later run boundary from the next start -- no key per entry.
 // KEYS (a template parameter, so the default values-only sort's variant carries none of the key
@@ -152,10 +154,12 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
   // entry positions are 32-bit (a sort holds < 2^31 entries, msm_launch_sort): one VGPR each
   const uint32_t valid = *valid_p;
   bool crossed = false;  // this thread left a head or tail partial (k_fix_level / k_bucket_fixup work)
+  bool grouped = false;  // ... and a level-1 group of 8 chunks lies inside one bucket (k_fix_level's)
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nchunks;
        t += (size_t)gridDim.x * blockDim.x) {
     const uint32_t a = (uint32_t)t * (uint32_t)acc_k;
-    if (a >= valid) continue;
+    uint32_t fb = 0xffffffffu, lb = 0xfffffffeu;  // the chunk's first / last bucket (none past valid)
+    if (a < valid) {
     const uint32_t b = a + acc_k < valid ? a + acc_k : valid;
     // a run is a head (it began before this chunk) iff it is the chunk's first run and entry
     // a - 1 has its bucket, a tail (it goes on after the chunk) iff it is the last run and entry
@@ -187,6 +191,8 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
         crossed |= (first && head_run) || (p >= b && tail);
         if (p >= b) {
           cbk[t] = make_uint2(first_bucket, cur);  // the buckets of entries a and b - 1 (k_fix_level)
+          fb = first_bucket;
+          lb = cur;
           break;
         }
         first = false;
@@ -211,10 +217,17 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
       for (int l = 0; l < 8; l++) q.y.v[l] = negy ? ny.v[l] : q.y.v[l];
       acc = xyzz_madd_lazy(acc, q);
     }
+    }
+    // k_fix_level's level-1 test for the group of chunks t .. t + 7 (t a multiple of 8: lane 8k):
+    // the first chunk's first bucket is the last chunk's last (every lane of the wave shuffles)
+    const uint32_t lb7 = __shfl_down(lb, 7, FIX_FAN);
+    grouped |= (threadIdx.x & (FIX_FAN - 1)) == 0 && t + FIX_FAN - 1 < nchunks && fb == lb7;
   }
-  // one flag per MSM: no run crossed a chunk (the 22-bit address commitment at C4: every bucket's
-  // four entries inside one chunk) -> the fixup levels have nothing to do
-  if (__any(crossed) && (threadIdx.x & 63) == 0) atomicOr(spans, 1u);
+  // two flags per MSM: no run crossed a chunk (the 22-bit address commitment at C4: every bucket's
+  // four entries inside one chunk) -> nothing to fix up; no 8-chunk group inside one bucket (any
+  // uniform scalars: the openings, C2) -> no fix level has a group to sum
+  const uint32_t f = (__any(crossed) ? 1u : 0u) | (__any(grouped) ? 2u : 0u);  // (every lane votes)
+  if (f && (threadIdx.x & 63) == 0) atomicOr(spans, f);
 }
 
 // Heavy buckets (skewed scalars: repeated values, small ranges) span many chunks; their
@@ -222,7 +235,6 @@ __global__ void __launch_bounds__(256) k_accumulate(const uint32_t *__restrict__
 // Level l >= 1, group g covers chunks [g F^l, (g+1) F^l) (F = FIX_FAN); its sum is formed only when
 // every sorted entry of those chunks has one key (then every head in it is a full-chunk
 // sum of that bucket); other groups are never read.
-constexpr int FIX_FAN = 8;  // short peel chains: single-thread add chains are latency-bound
 constexpr int FIX_LEVELS = 8;
 struct FixLevels {
   G1Xyzz *lv[FIX_LEVELS + 1];  // lv[l] for l >= 1 (the level-0 heads live in ht)
@@ -250,7 +262,9 @@ struct FixLevelArgs {
 __global__ void __launch_bounds__(256) k_fix_level(FixLevelArgs A, int level) {
   const FixLevelSet &S = A.s[blockIdx.y];
   const size_t n_groups = S.n_groups;
-  if (!n_groups || !S.valid[1]) return;  // (valid[1]: some run crossed a chunk, k_accumulate)
+  // (valid[1] bit 1: some 8-chunk group lies inside one bucket, k_accumulate; a group of any
+  // higher level is made of such groups)
+  if (!n_groups || !(S.valid[1] & 2u)) return;
   const size_t valid = *S.valid;
   const int acc_k = S.acc_k;
   const int j = threadIdx.x & (FIX_FAN - 1);
